@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark: 3D 7-point fp64 Jacobi (BASELINE.json metric, config 2 size per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one Jacobi sweep of the whole grid.  At N=1 the workload is
+BASELINE config 2 (512^3 interior, fp64, 7-point star; the default K=1000 is
+exactly its 1000 iterations).  At N>1 every rank owns a 512^3 Z-slab of a
+512 x 512 x 512N grid (weak scaling) and exchanges one halo plane with each
+neighbour per sweep over RCCL, overlapped with the interior sweep.
+
+Rank 0 prints one JSON line with the whole-job rate, the live roofline of the
+dominant kernel (algorithmic bytes per launch / average launch time from HIP
+events on the kernel's own stream), and a bounded CPU baseline (the oracle's
+single-thread restatement of the reference's naive sweep, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "Gcell-updates/s + achieved HBM GB/s vs roofline, 7-pt fp64 Jacobi, 1/2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, budget_s: float):
+    """The oracle (port of check_result's loop, stencil.cpp:94-131, generalised
+    to 3D) on the host, single-threaded like the reference, over a bounded
+    number of sweeps of the same 512^3 fp64 grid."""
+    from oracle import binding as ob
+    p = ob.problem(3, "fp64", "star", 1, "naive", n, n, n)
+    t1 = ob.timed_run(p, 1, threads=1)
+    iters = max(1, min(200, int(budget_s / max(t1, 1e-6))))
+    t = ob.timed_run(p, iters, threads=1)
+    cells = float(n) ** 3 * iters
+    return {"value": round(cells / t / 1e9, 4), "unit": "Gcell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ naive sweep, {n}^3 fp64 7-point, {iters} sweeps from the reference initial "
+                      f"condition, {t:.1f} s on 1 host thread"}
+
+
+def load_traffic(workload_key: str, kernel_name: str):
+    path = os.path.join(HERE, "profiles", "traffic.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    ent = data.get(workload_key, {}).get(kernel_name)
+    return ent.get("hbm_bytes_per_launch") if ent else None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from stencil_amd import _lib
+    from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
+    from stencil_amd.slab import SlabInfo, SlabJacobi, TorchDistExchanger
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n = args.n
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=1, order="naive", kernel=args.kernel)
+    eng = JacobiEngine(spec, n, n, n, device=local)
+    slab = SlabJacobi(eng, SlabInfo(rank, world, rank * n, n), TorchDistExchanger(rank, world),
+                      overlap=not args.no_overlap)
+    slab.init("reference")
+    launches_per_sweep_unit, kernel_id = eng.plan(2)
+    sweeps_per_launch = 2 // launches_per_sweep_unit  # 2 for TEMPORAL2, else 1
+    kname = {1: "direct", 2: "zmarch", 3: "temporal2"}[kernel_id]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---------------- warmup
+    if world == 1:
+        eng.iterate(args.warmup)
+    else:
+        slab.run(args.warmup)
+    barrier()
+
+    # ---------------- timed region: exactly K sweeps
+    stream = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    if world == 1:
+        _, dev_ms = eng.iterate(args.steps, stream=stream, timed=True)
+        kernel_ms_total = dev_ms
+        kernel_launches = eng.plan(args.steps)[0]
+    else:
+        slab.start_kernel_timing()
+        slab.run(args.steps)
+        kernel_ms_total, kernel_launches = slab.stop_kernel_timing()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    cells_per_gpu = float(n) ** 3
+    total_updates = cells_per_gpu * world * args.steps
+    gcell = total_updates / elapsed / 1e9
+    bytes_per_update = 2 * 8
+    # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
+    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (n - 2) / n
+    alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
+    launch_ms = kernel_ms_total / max(1, kernel_launches)
+    achieved = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        workload = f"3d7pt_fp64_{n}cube_per_gpu"
+        out = {
+            "metric": METRIC,
+            "value": round(gcell, 3),
+            "unit": "Gcell-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: the reference initial condition (x-ghost faces 1, everything else 0)",
+            "config": {
+                "workload": f"BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU "
+                            f"(global {n}x{n}x{n * world}), one step = one sweep",
+                "grid": [n, n, n * world],
+                "kernel": kname,
+                "parallelism": f"z-slab x{world}" + ("" if world == 1 else ", RCCL halo P2P overlapped"),
+                "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kname,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic(workload, kname),
+                "alg_bytes_per_launch": alg_bytes_launch,
+                "mean_launch_ms": round(launch_ms, 5),
+                "launches": kernel_launches,
+            },
+        }
+        try:
+            out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
+        except Exception as exc:  # calibration only
+            out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * stencil_hip.h -- the C-ABI boundary of the MI355X stencil engine
+ * (libstencil_hip.so, built from the .hip sources in stencil_amd/csrc for gfx950).
+ *
+ * Plain C: pointers, sizes and opaque stream handles only (a stream is a
+ * hipStream_t passed as void*; NULL = the default stream).  No HIP, torch or
+ * C++ types cross this boundary; the host CLI (stencil_amd/csrc/host) is
+ * compiled with plain g++ against this header alone.
+ *
+ * Two layers:
+ *
+ *  1. The reference's own kernel ABI, layout-compatible and name-identical
+ *     (drop-in for src/stencil/slave/stencil_slave.hpp:13-46):
+ *        void stencil_iterate_dma(StencilArguments*);                 (:28)
+ *        void stencil_iterate_dma_static_unroll(StencilArguments*);   (:33)
+ *        void stencil_iterate_dma_slave_pack(StencilArguments*);      (:41)
+ *        void stencil_iterate_rma(StencilArguments*);                 (:44)
+ *     In the reference these run on the 64 CPEs via
+ *     athread_spawn(SLAVE_FUN(fn), &args); athread_join()
+ *     (src/stencil/stencil.cpp:34-53).  Here the call runs the whole job on
+ *     the current GPU and returns when the parity-selected host buffer holds
+ *     the result.  Arithmetic order follows each reference variant so results
+ *     are bit-identical to what that variant computes.
+ *
+ *  2. The native engine API (device-resident grids, fp32/fp64, 2D/3D, star
+ *     and box shapes, any radius, slab sweeps for multi-GPU).  The reference
+ *     has no counterpart; it generalises Stencil::run
+ *     (src/stencil/stencil.cpp:23-57) and BoundaryMatrix
+ *     (include/stencil/boundary_matrix.hpp:31-238).
+ *
+ * Errors: native calls return STENCIL_OK (0) or a negative STENCIL_E* code;
+ * stencil_last_error_message() describes the most recent failure on the
+ * calling thread.  The reference-ABI entry points return void like the
+ * reference (stencil_slave.hpp:26-46) and report through
+ * stencil_last_error() (0 = success).
+ */
+#ifndef STENCIL_HIP_H
+#define STENCIL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+#define STENCIL_OK 0
+#define STENCIL_EINVAL (-1)      /* bad argument / unsupported combination */
+#define STENCIL_EHIP (-2)        /* a HIP runtime call failed */
+#define STENCIL_ENOMEM (-3)      /* device allocation failed */
+#define STENCIL_ENODEV (-4)      /* no usable gfx950 device */
+#define STENCIL_EUNSUPPORTED (-5)
+
+const char* stencil_strerror(int code);
+const char* stencil_last_error_message(void);
+int stencil_last_error(void);
+
+/* --------------------------------------------- 1. reference-compatible ABI */
+
+/* Layout-identical to detail::BoundaryMatrix<float,false>
+ * (include/stencil/boundary_matrix.hpp:225-237 field order, LP64: 40 bytes). */
+typedef struct StencilMatrixView {
+    size_t actual_width;      /* width + 2*boundary_width  (_actual_width)  */
+    size_t actual_height;     /* height + 2*boundary_height (_actual_height) */
+    unsigned boundary_width;  /* _boundary_width  (= radius) */
+    unsigned boundary_height; /* _boundary_height (= radius) */
+    size_t data_stride;       /* _data_stride, elements per row */
+    float* data;              /* _data, row-major incl. ghost ring, HOST memory */
+} StencilMatrixView;
+
+/* Layout-identical to struct Arguments (stencil_slave.hpp:13-24): 88 bytes. */
+typedef struct StencilArguments {
+    unsigned block_size; /* accepted for compatibility; the GPU picks its own tiling */
+    unsigned iterations;
+    StencilMatrixView input;  /* both buffers hold the initial grid + ghosts */
+    StencilMatrixView output; /* final grid: output if iterations odd, else input */
+} StencilArguments;
+
+void stencil_iterate_dma(StencilArguments* args);
+void stencil_iterate_dma_static_unroll(StencilArguments* args);
+void stencil_iterate_dma_slave_pack(StencilArguments* args);
+void stencil_iterate_rma(StencilArguments* args);
+
+/* ------------------------------------------------------ 2. native engine */
+
+enum { STENCIL_F32 = 0, STENCIL_F64 = 1 };
+enum { STENCIL_STAR = 0, STENCIL_BOX = 1 };
+/* Sum order. NAIVE = Stencil::check_result (stencil.cpp:104-125) and
+ * DMAStaticUnroll; DMA = stencil_dma.cpp (r=1: 431-444, r>1: 636-650).
+ * DMA order exists for 2D star only. */
+enum { STENCIL_ORDER_NAIVE = 0, STENCIL_ORDER_DMA = 1 };
+/* Kernel family. AUTO picks the fastest one that supports the problem. */
+enum {
+    STENCIL_KERNEL_AUTO = 0,
+    STENCIL_KERNEL_DIRECT = 1,    /* one cell per lane, neighbours via L1/L2 */
+    STENCIL_KERNEL_ZMARCH = 2,    /* 2.5D: LDS plane + z register queue */
+    STENCIL_KERNEL_TEMPORAL2 = 3  /* ZMARCH with 2 fused time steps per launch */
+};
+enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
+
+typedef struct stencil_problem {
+    int32_t dims;   /* 2 or 3 */
+    int32_t dtype;  /* STENCIL_F32 / STENCIL_F64 */
+    int32_t shape;  /* STENCIL_STAR / STENCIL_BOX */
+    int32_t radius; /* >= 1 (reference -r) */
+    int32_t order;  /* STENCIL_ORDER_* */
+    int32_t kernel; /* STENCIL_KERNEL_* */
+    int64_t nx, ny, nz; /* interior extents (reference: width = height = -s); nz = 1 for 2D */
+} stencil_problem;
+
+/* Device layout: x fastest, ghost ring of width `radius` on every axis the
+ * problem has, rows padded so interior x = 0 of every row is 128-byte aligned.
+ * Element (x, y, z) of the interior (ghosts at -r..-1 and n..n+r-1) is at
+ *   base[origin + z*plane + y*row + x]    (z = 0 for 2D). */
+typedef struct stencil_layout {
+    stencil_problem prob;
+    int64_t row;    /* elements between consecutive rows (y) */
+    int64_t plane;  /* elements between consecutive planes (z); rows*row */
+    int64_t planes; /* allocated planes (nz + 2r for 3D, 1 for 2D) */
+    int64_t rows;   /* allocated rows per plane (ny + 2r) */
+    int64_t origin; /* element offset of interior (0,0,0) */
+    int64_t elems;  /* elements to allocate */
+    int64_t bytes;  /* elems * sizeof(element) */
+} stencil_layout;
+
+int stencil_layout_init(const stencil_problem* prob, stencil_layout* out);
+
+/* Extent of the slow axis (z for 3D, y for 2D): sweeps and slabs range over it. */
+int64_t stencil_slow_extent(const stencil_layout* l);
+
+int stencil_device_count(int* count);
+int stencil_set_device(int device);
+int stencil_synchronize(void* stream);
+int stencil_alloc(const stencil_layout* l, void** dev);
+int stencil_free(void* dev);
+
+/* Initial condition on the device (interior + ghosts), see DESIGN.md §Init:
+ * REFERENCE = stencil.cpp:190-207 (x-ghosts 1, every other cell 0);
+ * RANDOM    = interior splitmix64(seed + linear index) in [0,1). */
+int stencil_fill_initial(const stencil_layout* l, void* dev, int init_kind, uint64_t seed,
+                         void* stream);
+
+/* Host <-> device copies of the whole ghost-padded grid. The host array is
+ * dense: row stride host_row elements, host_rows rows per plane (the
+ * reference's BoundaryMatrix has host_row = n + 2r). Asynchronous on
+ * `stream` (host memory should be pinned for true overlap). */
+int stencil_upload(const stencil_layout* l, void* dev, const void* host, int64_t host_row,
+                   int64_t host_rows, void* stream);
+int stencil_download(const stencil_layout* l, const void* dev, void* host, int64_t host_row,
+                     int64_t host_rows, void* stream);
+/* Copy `count` planes (slow-axis units, ghost rows/planes included, indices
+ * relative to the interior: -r .. n+r-1) between two device grids. */
+int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_first,
+                        void* dst, int64_t dst_first, int64_t count, void* stream);
+
+/* One Jacobi sweep out = S(in) over slow-axis interior indices [begin, end).
+ * Ghost cells are read, never written. */
+int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                  void* stream);
+
+/* Two fused sweeps (TEMPORAL2 family): out = S(S(in)) on [begin, end), using
+ * `in`'s ghost/halo planes (2r deep) for the redundant halo compute. `out`
+ * must differ from `in`; no scratch grid is needed. */
+int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                   void* stream);
+
+/* Whole job: `iterations` ping-pong sweeps starting from grid `a` (grid `b`
+ * must hold the same ghosts). *final_in_b = 1 when the result is in `b`
+ * (iterations odd), 0 when in `a` (parity rule, stencil.cpp:88-92,134).
+ * With prob.kernel == TEMPORAL2, pairs of iterations run as one launch.
+ * If elapsed_ms is non-NULL the call brackets its launches with hipEvents on
+ * `stream`, synchronises, and stores the elapsed device time. */
+int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iterations, void* stream,
+                    int* final_in_b, float* elapsed_ms);
+
+/* Launch plan of stencil_iterate for `iterations`: number of kernel launches
+ * and the kernel family AUTO resolves to. */
+int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches,
+                 int32_t* kernel);
+
+/* Device-side checksums of the interior: per-plane sums (double, ascending
+ * x, y order within the plane) written to `plane_sums` (slow_extent
+ * entries, device or host pointer) -- the "checksum of checksums" used by
+ * the full-size property tests. */
+int stencil_plane_sums(const stencil_layout* l, const void* dev, double* plane_sums_host,
+                       void* stream);
+
+/* A plain device copy kernel (read n bytes, write n bytes) used by bench.py to
+ * calibrate attainable HBM bandwidth on the box. */
+int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, void* stream,
+                           float* elapsed_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STENCIL_HIP_H */

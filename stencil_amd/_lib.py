@@ -1,0 +1,131 @@
+"""ctypes binding of libstencil_hip.so (include/stencil_hip.h).
+
+The shared library is the product: every sweep runs as a gfx950 HIP kernel
+behind the C-ABI.  There is no Python or CPU fallback; if the library is
+missing or cannot be loaded this module raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstencil_hip.so")
+
+STENCIL_OK = 0
+F32, F64 = 0, 1
+STAR, BOX = 0, 1
+ORDER_NAIVE, ORDER_DMA = 0, 1
+KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2 = 0, 1, 2, 3
+INIT_REFERENCE, INIT_RANDOM = 0, 1
+
+KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2}
+
+# Every symbol include/stencil_hip.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "stencil_strerror", "stencil_last_error_message", "stencil_last_error",
+    "stencil_iterate_dma", "stencil_iterate_dma_static_unroll", "stencil_iterate_dma_slave_pack",
+    "stencil_iterate_rma",
+    "stencil_layout_init", "stencil_slow_extent", "stencil_device_count", "stencil_set_device",
+    "stencil_synchronize", "stencil_alloc", "stencil_free", "stencil_fill_initial", "stencil_upload",
+    "stencil_download", "stencil_copy_planes", "stencil_sweep", "stencil_sweep2", "stencil_iterate",
+    "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth",
+)
+
+
+class Problem(Structure):
+    _fields_ = [("dims", c_int32), ("dtype", c_int32), ("shape", c_int32), ("radius", c_int32),
+                ("order", c_int32), ("kernel", c_int32), ("nx", c_int64), ("ny", c_int64), ("nz", c_int64)]
+
+
+class Layout(Structure):
+    _fields_ = [("prob", Problem), ("row", c_int64), ("plane", c_int64), ("planes", c_int64),
+                ("rows", c_int64), ("origin", c_int64), ("elems", c_int64), ("bytes", c_int64)]
+
+
+class MatrixView(Structure):
+    """Layout of detail::BoundaryMatrix<float,false> (boundary_matrix.hpp:225-237)."""
+    _fields_ = [("actual_width", ctypes.c_size_t), ("actual_height", ctypes.c_size_t),
+                ("boundary_width", ctypes.c_uint), ("boundary_height", ctypes.c_uint),
+                ("data_stride", ctypes.c_size_t), ("data", POINTER(c_float))]
+
+
+class Arguments(Structure):
+    """Layout of struct Arguments (stencil_slave.hpp:13-24)."""
+    _fields_ = [("block_size", ctypes.c_uint), ("iterations", ctypes.c_uint),
+                ("input", MatrixView), ("output", MatrixView)]
+
+
+class StencilError(RuntimeError):
+    def __init__(self, code: int, where: str, message: str):
+        super().__init__(f"{where}: error {code}: {message}")
+        self.code = code
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libstencil_hip.so once; raise if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP extension has not been built "
+            "(run `make` or `python -c 'import __graft_entry__ as g; g.build()'`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, L = POINTER(Problem), POINTER(Layout)
+    sig = {
+        "stencil_strerror": (c_char_p, [c_int]),
+        "stencil_last_error_message": (c_char_p, []),
+        "stencil_last_error": (c_int, []),
+        "stencil_layout_init": (c_int, [P, L]),
+        "stencil_slow_extent": (c_int64, [L]),
+        "stencil_device_count": (c_int, [POINTER(c_int)]),
+        "stencil_set_device": (c_int, [c_int]),
+        "stencil_synchronize": (c_int, [c_void_p]),
+        "stencil_alloc": (c_int, [L, POINTER(c_void_p)]),
+        "stencil_free": (c_int, [c_void_p]),
+        "stencil_fill_initial": (c_int, [L, c_void_p, c_int, c_uint64, c_void_p]),
+        "stencil_upload": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_download": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_copy_planes": (c_int, [L, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_sweep": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_sweep2": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_iterate": (c_int, [L, c_void_p, c_void_p, c_uint32, c_void_p, POINTER(c_int), POINTER(c_float)]),
+        "stencil_plan": (c_int, [L, c_uint32, POINTER(c_int64), POINTER(c_int32)]),
+        "stencil_plane_sums": (c_int, [L, c_void_p, POINTER(c_double), c_void_p]),
+        "stencil_copy_bandwidth": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, POINTER(c_float)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    for name in ("stencil_iterate_dma", "stencil_iterate_dma_static_unroll",
+                 "stencil_iterate_dma_slave_pack", "stencil_iterate_rma"):
+        fn = getattr(lib, name)
+        fn.restype = None
+        fn.argtypes = [POINTER(Arguments)]
+    _lib = lib
+    return lib
+
+
+def check(rc: int, where: str) -> None:
+    if rc != STENCIL_OK:
+        lib = load()
+        msg = (lib.stencil_last_error_message() or b"").decode(errors="replace")
+        raise StencilError(rc, where, msg or lib.stencil_strerror(rc).decode())
+
+
+def make_problem(dims=3, dtype=F64, shape=STAR, radius=1, order=ORDER_NAIVE, kernel=KERNEL_AUTO,
+                 nx=1, ny=1, nz=1) -> Problem:
+    return Problem(dims, dtype, shape, radius, order, kernel, nx, ny, nz if dims == 3 else 1)
+
+
+def make_layout(prob: Problem) -> Layout:
+    lib = load()
+    lay = Layout()
+    check(lib.stencil_layout_init(ctypes.byref(prob), ctypes.byref(lay)), "stencil_layout_init")
+    return lay

@@ -1,0 +1,490 @@
+// api.hip -- the C-ABI of libstencil_hip.so (declared in include/stencil_hip.h).
+//
+// Host-side orchestration: layout, allocation, initial condition, transfers,
+// kernel-family dispatch, the ping-pong iteration loop, and the
+// reference-compatible entry points stencil_iterate_{dma, dma_static_unroll,
+// dma_slave_pack, rma} that replace the Sunway CPE kernels
+// (src/stencil/slave/stencil_slave.hpp:26-46).
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "common.hpp"
+
+namespace stencil {
+
+namespace {
+thread_local int g_last_code = STENCIL_OK;
+thread_local char g_last_msg[512] = "";
+}  // namespace
+
+int set_error(int code, const char* fmt, ...) {
+    g_last_code = code;
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(g_last_msg, sizeof g_last_msg, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+void clear_error() {
+    g_last_code = STENCIL_OK;
+    g_last_msg[0] = '\0';
+}
+
+namespace {
+
+inline size_t elem_size(const stencil_problem& p) { return p.dtype == STENCIL_F32 ? 4 : 8; }
+
+int check_problem(const stencil_problem* p) {
+    if (!p) return set_error(STENCIL_EINVAL, "null problem");
+    if (p->dims != 2 && p->dims != 3) return set_error(STENCIL_EINVAL, "dims must be 2 or 3 (got %d)", p->dims);
+    if (p->dtype != STENCIL_F32 && p->dtype != STENCIL_F64) return set_error(STENCIL_EINVAL, "bad dtype %d", p->dtype);
+    if (p->shape != STENCIL_STAR && p->shape != STENCIL_BOX) return set_error(STENCIL_EINVAL, "bad shape %d", p->shape);
+    if (p->radius < 1 || p->radius > 64) return set_error(STENCIL_EINVAL, "radius must be in [1, 64] (got %d)", p->radius);
+    if (p->order != STENCIL_ORDER_NAIVE && p->order != STENCIL_ORDER_DMA) return set_error(STENCIL_EINVAL, "bad order %d", p->order);
+    if (p->order == STENCIL_ORDER_DMA && (p->dims != 2 || p->shape != STENCIL_STAR))
+        return set_error(STENCIL_EINVAL, "DMA sum order is defined for 2D star stencils only");
+    if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_TEMPORAL2) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
+    if (p->nx < 0 || p->ny < 0 || p->nz < 0) return set_error(STENCIL_EINVAL, "negative extent");
+    if (p->dims == 2 && p->nz != 1) return set_error(STENCIL_EINVAL, "2D problems need nz = 1");
+    if (p->kernel == STENCIL_KERNEL_ZMARCH && !zmarch_supports(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "ZMARCH kernel supports 3D star r=1 naive order only");
+    if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !temporal2_supports(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 kernel does not support this problem");
+    return STENCIL_OK;
+}
+
+int check_layout(const stencil_layout* l) {
+    if (!l) return set_error(STENCIL_EINVAL, "null layout");
+    return check_problem(&l->prob);
+}
+
+// Resolve AUTO to a concrete single-sweep kernel family.
+int sweep_family(const stencil_problem& p) {
+    if (p.kernel == STENCIL_KERNEL_DIRECT) return STENCIL_KERNEL_DIRECT;
+    if (zmarch_supports(p)) return STENCIL_KERNEL_ZMARCH;
+    return STENCIL_KERNEL_DIRECT;
+}
+
+inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+// ---- initial condition ----------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ void u01(uint64_t u, float& f) { f = float(u >> 40) * 0x1.0p-24f; }
+__device__ __forceinline__ void u01(uint64_t u, double& d) { d = double(u >> 11) * 0x1.0p-53; }
+
+// One thread per allocated element.  Padding columns (outside the ghost
+// ring) get 0; ghost cells follow stencil.cpp:190-207 generalised to 3D.
+template <typename T>
+__global__ void fill_initial_kernel(T* __restrict__ buf, Geom g, int64_t elems, int64_t row,
+                                    int64_t rows, int64_t origin_x, int r, int dims, int kind,
+                                    uint64_t seed) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= elems) return;
+    const int64_t pz = i / (row * rows);
+    const int64_t rem = i - pz * row * rows;
+    const int64_t py = rem / row;
+    const int64_t px = rem - py * row;
+    const int64_t x = px - origin_x, y = py - r, z = dims == 3 ? pz - r : 0;
+    T v = T(0);
+    const bool in_x = x >= -r && x < g.nx + r;
+    if (in_x) {
+        const bool xghost = x < 0 || x >= g.nx;
+        const bool interior = !xghost && y >= 0 && y < g.ny && z >= 0 && z < g.nz;
+        if (xghost) {
+            v = T(1);
+        } else if (interior && kind == STENCIL_INIT_RANDOM) {
+            const uint64_t lin = (uint64_t(z) * uint64_t(g.ny) + uint64_t(y)) * uint64_t(g.nx) + uint64_t(x);
+            u01(splitmix64(seed + lin), v);
+        }
+    }
+    buf[i] = v;
+}
+
+// Deterministic per-plane sums: one workgroup per slow-axis index, fixed
+// lane -> element mapping and a fixed tree, so equal grids give equal bits.
+template <typename T>
+__global__ void __launch_bounds__(256) plane_sums_kernel(const T* __restrict__ buf, Geom g, int dims,
+                                                         double* __restrict__ out) {
+    __shared__ double red[256];
+    const int64_t s = blockIdx.x;
+    const int64_t ny = dims == 3 ? g.ny : 1;
+    const int64_t base = g.origin + (dims == 3 ? s * g.plane : s * g.row);
+    double acc = 0.0;
+    for (int64_t y = 0; y < ny; ++y)
+        for (int64_t x = threadIdx.x; x < g.nx; x += 256) acc += double(buf[base + y * g.row + x]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (int(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[s] = red[0];
+}
+
+__global__ void __launch_bounds__(256) copy_kernel(float4* __restrict__ dst, const float4* __restrict__ src,
+                                                   int64_t n) {
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+// Host pointer of the first allocated element of plane `p` (slow-axis
+// index, relative to the interior) and of its ghost corner.
+inline int64_t ghost_corner(const stencil_layout& l) {
+    const int r = l.prob.radius;
+    return l.origin - int64_t(r) * l.row - r - (l.prob.dims == 3 ? int64_t(r) * l.plane : 0);
+}
+
+}  // namespace
+}  // namespace stencil
+
+using namespace stencil;
+
+extern "C" {
+
+const char* stencil_strerror(int code) {
+    switch (code) {
+    case STENCIL_OK: return "success";
+    case STENCIL_EINVAL: return "invalid argument";
+    case STENCIL_EHIP: return "HIP runtime error";
+    case STENCIL_ENOMEM: return "out of device memory";
+    case STENCIL_ENODEV: return "no usable GPU";
+    case STENCIL_EUNSUPPORTED: return "unsupported combination";
+    default: return "unknown error";
+    }
+}
+
+const char* stencil_last_error_message(void) { return g_last_msg; }
+int stencil_last_error(void) { return g_last_code; }
+
+int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
+    if (int rc = check_problem(prob)) return rc;
+    if (!out) return set_error(STENCIL_EINVAL, "null layout");
+    const stencil_problem& p = *prob;
+    const int64_t r = p.radius;
+    const int64_t align = 128 / int64_t(elem_size(p));  // elements per 128 B
+    const int64_t origin_x = (r + align - 1) / align * align;
+    stencil_layout l{};
+    l.prob = p;
+    l.row = (origin_x + p.nx + r + align - 1) / align * align;
+    l.rows = p.ny + 2 * r;
+    l.plane = l.row * l.rows;
+    l.planes = p.dims == 3 ? p.nz + 2 * r : 1;
+    l.origin = (p.dims == 3 ? r * l.plane : 0) + r * l.row + origin_x;
+    l.elems = l.plane * l.planes;
+    l.bytes = l.elems * int64_t(elem_size(p));
+    *out = l;
+    clear_error();
+    return STENCIL_OK;
+}
+
+int64_t stencil_slow_extent(const stencil_layout* l) {
+    return l->prob.dims == 3 ? l->prob.nz : l->prob.ny;
+}
+
+int stencil_device_count(int* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (count) *count = n;
+    if (n == 0) return set_error(STENCIL_ENODEV, "no HIP device visible");
+    return STENCIL_OK;
+}
+
+int stencil_set_device(int device) {
+    STENCIL_HIP_CHECK(hipSetDevice(device));
+    return STENCIL_OK;
+}
+
+int stencil_synchronize(void* stream) {
+    STENCIL_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+    return STENCIL_OK;
+}
+
+int stencil_alloc(const stencil_layout* l, void** dev) {
+    if (int rc = check_layout(l)) return rc;
+    if (!dev) return set_error(STENCIL_EINVAL, "null out pointer");
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, size_t(l->bytes) + 256);  // tail pad for vector over-reads
+    if (e != hipSuccess) return set_error(STENCIL_ENOMEM, "hipMalloc(%lld) failed: %s", (long long)l->bytes, hipGetErrorString(e));
+    *dev = p;
+    return STENCIL_OK;
+}
+
+int stencil_free(void* dev) {
+    STENCIL_HIP_CHECK(hipFree(dev));
+    return STENCIL_OK;
+}
+
+int stencil_fill_initial(const stencil_layout* l, void* dev, int init_kind, uint64_t seed, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (init_kind != STENCIL_INIT_REFERENCE && init_kind != STENCIL_INIT_RANDOM)
+        return set_error(STENCIL_EINVAL, "bad init kind %d", init_kind);
+    const Geom g = geom_of(*l);
+    const int64_t r = l->prob.radius;
+    const int64_t origin_x = l->origin - r * l->row - (l->prob.dims == 3 ? r * l->plane : 0);
+    const int64_t blocks = (l->elems + 255) / 256;
+    if (l->prob.dtype == STENCIL_F32)
+        hipLaunchKernelGGL(fill_initial_kernel<float>, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream),
+                           static_cast<float*>(dev), g, l->elems, l->row, l->rows, origin_x, int(r),
+                           l->prob.dims, init_kind, seed);
+    else
+        hipLaunchKernelGGL(fill_initial_kernel<double>, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream),
+                           static_cast<double*>(dev), g, l->elems, l->row, l->rows, origin_x, int(r),
+                           l->prob.dims, init_kind, seed);
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
+static int copy_grid(const stencil_layout* l, void* dev, const void* host_src, void* host_dst,
+                     int64_t host_row, int64_t host_rows, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    const stencil_problem& p = l->prob;
+    const int64_t r = p.radius;
+    const size_t es = elem_size(p);
+    const int64_t width = p.nx + 2 * r, height = p.ny + 2 * r;
+    if (host_row < width || host_rows < height) return set_error(STENCIL_EINVAL, "host array too small");
+    const int64_t corner = ghost_corner(*l);
+    for (int64_t z = 0; z < l->planes; ++z) {
+        char* d = static_cast<char*>(dev) + size_t(corner + z * l->plane) * es;
+        if (host_src) {
+            const char* h = static_cast<const char*>(host_src) + size_t(z * host_row * host_rows) * es;
+            STENCIL_HIP_CHECK(hipMemcpy2DAsync(d, size_t(l->row) * es, h, size_t(host_row) * es, size_t(width) * es,
+                                               size_t(height), hipMemcpyHostToDevice, as_stream(stream)));
+        } else {
+            char* h = static_cast<char*>(host_dst) + size_t(z * host_row * host_rows) * es;
+            STENCIL_HIP_CHECK(hipMemcpy2DAsync(h, size_t(host_row) * es, d, size_t(l->row) * es, size_t(width) * es,
+                                               size_t(height), hipMemcpyDeviceToHost, as_stream(stream)));
+        }
+    }
+    return STENCIL_OK;
+}
+
+int stencil_upload(const stencil_layout* l, void* dev, const void* host, int64_t host_row, int64_t host_rows,
+                   void* stream) {
+    return copy_grid(l, dev, host, nullptr, host_row, host_rows, stream);
+}
+
+int stencil_download(const stencil_layout* l, const void* dev, void* host, int64_t host_row, int64_t host_rows,
+                     void* stream) {
+    return copy_grid(l, const_cast<void*>(dev), nullptr, host, host_row, host_rows, stream);
+}
+
+int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_first, void* dst, int64_t dst_first,
+                        int64_t count, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    const int64_t r = l->prob.radius;
+    const int64_t n = stencil_slow_extent(l);
+    if (count < 0 || src_first < -r || dst_first < -r || src_first + count > n + r || dst_first + count > n + r)
+        return set_error(STENCIL_EINVAL, "plane range out of bounds");
+    const size_t es = elem_size(l->prob);
+    const int64_t unit = l->prob.dims == 3 ? l->plane : l->row;
+    // First allocated element of slow-axis index k: for 3D the whole plane,
+    // for 2D the whole padded row.
+    const int64_t base = l->prob.dims == 3 ? r * l->plane : (l->origin - (l->origin % l->row));
+    const char* s = static_cast<const char*>(src) + size_t(base + src_first * unit) * es;
+    char* d = static_cast<char*>(dst) + size_t(base + dst_first * unit) * es;
+    if (count == 0) return STENCIL_OK;
+    STENCIL_HIP_CHECK(hipMemcpyAsync(d, s, size_t(count * unit) * es, hipMemcpyDeviceToDevice, as_stream(stream)));
+    return STENCIL_OK;
+}
+
+int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range [%lld, %lld) out of bounds", (long long)begin, (long long)end);
+    if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported (Jacobi ping-pong)");
+    int rc;
+    if (sweep_family(l->prob) == STENCIL_KERNEL_ZMARCH)
+        rc = launch_zmarch(*l, in, out, begin, end, as_stream(stream));
+    else
+        rc = launch_direct(*l, in, out, begin, end, as_stream(stream));
+    if (rc == STENCIL_OK) clear_error();
+    return rc;
+}
+
+int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (!temporal2_supports(l->prob)) return set_error(STENCIL_EUNSUPPORTED, "no fused two-step kernel for this problem");
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range out of bounds");
+    if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
+    int rc = launch_temporal2(*l, in, out, begin, end, as_stream(stream));
+    if (rc == STENCIL_OK) clear_error();
+    return rc;
+}
+
+int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {
+    if (int rc = check_layout(l)) return rc;
+    const bool t2 = l->prob.kernel == STENCIL_KERNEL_TEMPORAL2;
+    if (launches) *launches = t2 ? int64_t(iterations / 2 + iterations % 2) : int64_t(iterations);
+    if (kernel) *kernel = t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
+    return STENCIL_OK;
+}
+
+int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iterations, void* stream, int* final_in_b,
+                    float* elapsed_ms) {
+    if (int rc = check_layout(l)) return rc;
+    if (!a || !b || a == b) return set_error(STENCIL_EINVAL, "need two distinct grids");
+    hipStream_t s = as_stream(stream);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (elapsed_ms) {
+        STENCIL_HIP_CHECK(hipEventCreate(&e0));
+        STENCIL_HIP_CHECK(hipEventCreate(&e1));
+        STENCIL_HIP_CHECK(hipEventRecord(e0, s));
+    }
+    const int64_t n = stencil_slow_extent(l);
+    const bool t2 = l->prob.kernel == STENCIL_KERNEL_TEMPORAL2;
+    void* in = a;
+    void* out = b;
+    bool swapped = false;
+    uint32_t i = 0;
+    int rc = STENCIL_OK;
+    if (t2) {
+        // A fused pair reads `in` and writes S(S(in)) to `out`, so the buffer
+        // holding the result no longer follows the one-sweep parity rule; the
+        // caller learns where it is through *final_in_b.
+        for (; i + 2 <= iterations && rc == STENCIL_OK; i += 2) {
+            rc = launch_temporal2(*l, in, out, 0, n, s);
+            std::swap(in, out);
+            swapped = !swapped;
+        }
+    }
+    for (; i < iterations && rc == STENCIL_OK; ++i) {
+        rc = sweep_family(l->prob) == STENCIL_KERNEL_ZMARCH ? launch_zmarch(*l, in, out, 0, n, s)
+                                                             : launch_direct(*l, in, out, 0, n, s);
+        std::swap(in, out);
+        swapped = !swapped;
+    }
+    if (rc != STENCIL_OK) return rc;
+    if (final_in_b) *final_in_b = in == b ? 1 : 0;
+    if (elapsed_ms) {
+        STENCIL_HIP_CHECK(hipEventRecord(e1, s));
+        STENCIL_HIP_CHECK(hipEventSynchronize(e1));
+        STENCIL_HIP_CHECK(hipEventElapsedTime(elapsed_ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    (void)swapped;
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_plane_sums(const stencil_layout* l, const void* dev, double* plane_sums_host, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    const int64_t n = stencil_slow_extent(l);
+    if (n == 0) return STENCIL_OK;
+    double* d = nullptr;
+    STENCIL_HIP_CHECK(hipMalloc(&d, size_t(n) * sizeof(double)));
+    const Geom g = geom_of(*l);
+    if (l->prob.dtype == STENCIL_F32)
+        hipLaunchKernelGGL(plane_sums_kernel<float>, dim3(unsigned(n)), dim3(256), 0, as_stream(stream),
+                           static_cast<const float*>(dev), g, l->prob.dims, d);
+    else
+        hipLaunchKernelGGL(plane_sums_kernel<double>, dim3(unsigned(n)), dim3(256), 0, as_stream(stream),
+                           static_cast<const double*>(dev), g, l->prob.dims, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(plane_sums_host, d, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_error(STENCIL_EHIP, "plane sums failed: %s", hipGetErrorString(e));
+    return STENCIL_OK;
+}
+
+int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, void* stream, float* elapsed_ms) {
+    if (!dst || !src || bytes <= 0 || (bytes % 16) != 0 || reps <= 0) return set_error(STENCIL_EINVAL, "bad copy args");
+    hipStream_t s = as_stream(stream);
+    hipEvent_t e0, e1;
+    STENCIL_HIP_CHECK(hipEventCreate(&e0));
+    STENCIL_HIP_CHECK(hipEventCreate(&e1));
+    const int64_t n = bytes / 16;
+    const unsigned blocks = unsigned(std::min<int64_t>((n + 255) / 256, 256 * 16));
+    STENCIL_HIP_CHECK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, s, static_cast<float4*>(dst),
+                           static_cast<const float4*>(src), n);
+    STENCIL_LAUNCH_CHECK();
+    STENCIL_HIP_CHECK(hipEventRecord(e1, s));
+    STENCIL_HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    STENCIL_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (elapsed_ms) *elapsed_ms = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return STENCIL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Reference-compatible entry points (stencil_slave.hpp:26-46).
+//
+// The Sunway kernels read `input`, sweep `iterations` times, and leave the
+// final grid in `output` when the count is odd and in `input` when it is even
+// (stencil_dma.cpp:556-557,567; stencil.cpp:88-92,134).  Ghost cells are
+// never written.  Here: both host grids go to HBM, the GPU sweeps, the final
+// grid comes back into the parity-selected host buffer.
+// ---------------------------------------------------------------------------
+static void reference_entry(StencilArguments* args, int order) {
+    clear_error();
+    if (!args) { set_error(STENCIL_EINVAL, "null arguments"); return; }
+    const StencilMatrixView& in = args->input;
+    const StencilMatrixView& out = args->output;
+    if (in.boundary_width != in.boundary_height || in.boundary_width == 0) {
+        set_error(STENCIL_EINVAL, "boundary width and height must be equal and >= 1");
+        return;
+    }
+    if (in.actual_width != out.actual_width || in.actual_height != out.actual_height ||
+        in.boundary_width != out.boundary_width || in.data_stride != out.data_stride) {
+        set_error(STENCIL_EINVAL, "input and output views differ in shape");
+        return;
+    }
+    const int r = int(in.boundary_width);
+    if (in.actual_width < size_t(2 * r) || in.actual_height < size_t(2 * r)) {
+        set_error(STENCIL_EINVAL, "view smaller than its ghost ring");
+        return;
+    }
+    stencil_problem p{};
+    p.dims = 2;
+    p.dtype = STENCIL_F32;
+    p.shape = STENCIL_STAR;
+    p.radius = r;
+    p.order = order;
+    p.kernel = STENCIL_KERNEL_AUTO;
+    p.nx = int64_t(in.actual_width) - 2 * r;
+    p.ny = int64_t(in.actual_height) - 2 * r;
+    p.nz = 1;
+    if (p.nx == 0 || p.ny == 0) return;  // empty blocks return silently (stencil_dma.cpp:413-415)
+    stencil_layout l;
+    if (stencil_layout_init(&p, &l)) return;
+    void* a = nullptr;
+    void* b = nullptr;
+    if (stencil_alloc(&l, &a)) return;
+    if (stencil_alloc(&l, &b)) { (void)hipFree(a); return; }
+    int final_in_b = 0;
+    int rc = stencil_upload(&l, a, in.data, int64_t(in.data_stride), int64_t(in.actual_height), nullptr);
+    if (!rc) rc = stencil_upload(&l, b, out.data, int64_t(out.data_stride), int64_t(out.actual_height), nullptr);
+    if (!rc) rc = stencil_iterate(&l, a, b, args->iterations, nullptr, &final_in_b, nullptr);
+    if (!rc) {
+        const StencilMatrixView& dst = (args->iterations & 1u) ? out : in;
+        rc = stencil_download(&l, final_in_b ? b : a, dst.data, int64_t(dst.data_stride), int64_t(dst.actual_height), nullptr);
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) set_error(STENCIL_EHIP, "synchronize: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+}
+
+void stencil_iterate_dma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
+void stencil_iterate_dma_static_unroll(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_NAIVE); }
+void stencil_iterate_dma_slave_pack(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
+void stencil_iterate_rma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// common.hpp -- shared device/host definitions for libstencil_hip.so (gfx950).
+//
+// Everything here is internal to the library; the public boundary is
+// include/stencil_hip.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "stencil_hip.h"
+
+namespace stencil {
+
+// Geometry handed to kernels by value (SGPR-resident).
+struct Geom {
+    int64_t nx, ny, nz;  // interior extents (nz = 1 for 2D)
+    int64_t row;         // row stride (elements)
+    int64_t plane;       // plane stride (elements)
+    int64_t origin;      // element offset of interior (0,0,0)
+};
+
+inline Geom geom_of(const stencil_layout& l) {
+    return Geom{l.prob.nx, l.prob.ny, l.prob.nz, l.row, l.plane, l.origin};
+}
+
+// Record an error for stencil_last_error_message(); returns `code`.
+int set_error(int code, const char* fmt, ...);
+// Clear the per-thread error state (success).
+void clear_error();
+
+#define STENCIL_HIP_CHECK(expr)                                                              \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return ::stencil::set_error(STENCIL_EHIP, "%s failed: %s (%s:%d)", #expr,        \
+                                        hipGetErrorString(e_), __FILE__, __LINE__);          \
+    } while (0)
+
+#define STENCIL_LAUNCH_CHECK()                                                               \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess)                                                                \
+            return ::stencil::set_error(STENCIL_EHIP, "kernel launch failed: %s (%s:%d)",    \
+                                        hipGetErrorString(e_), __FILE__, __LINE__);          \
+    } while (0)
+
+// Averaging weight, computed on the host in the element type so the IEEE
+// division is the same correctly-rounded one the reference performs
+// (stencil.cpp:85-86: 1.f / float((bw + bh) * 2)).
+template <typename T>
+inline T avg_weight(const stencil_problem& p) {
+    if (p.shape == STENCIL_BOX) {
+        int64_t w = 2 * int64_t(p.radius) + 1, n = w * w;
+        if (p.dims == 3) n *= w;
+        return T(1) / T(n - 1);
+    }
+    return T(1) / T(2 * p.dims * p.radius);
+}
+
+// ---- kernel entry points (defined in kernels_*.hip) ----------------------
+int launch_direct(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
+                  hipStream_t s);
+int launch_zmarch(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
+                  hipStream_t s);
+int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t begin,
+                     int64_t end, hipStream_t s);
+bool zmarch_supports(const stencil_problem& p);
+bool temporal2_supports(const stencil_problem& p);
+
+}  // namespace stencil

@@ -1,0 +1,215 @@
+// stencil.cpp -- host engine (mirror of src/stencil/stencil.cpp).
+#include "stencil.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+
+#include "stencil_hip.h"
+
+namespace {
+
+void check(int rc, const char* what) {
+    if (rc != STENCIL_OK)
+        throw std::runtime_error(std::string(what) + ": " + stencil_strerror(rc) + ": " +
+                                 stencil_last_error_message());
+}
+
+int kernel_of(const std::string& k) {
+    if (k == "direct") return STENCIL_KERNEL_DIRECT;
+    if (k == "zmarch") return STENCIL_KERNEL_ZMARCH;
+    if (k == "temporal2") return STENCIL_KERNEL_TEMPORAL2;
+    return STENCIL_KERNEL_AUTO;
+}
+
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+void u01(uint64_t u, float& f) { f = float(u >> 40) * 0x1.0p-24f; }
+void u01(uint64_t u, double& d) { d = double(u >> 11) * 0x1.0p-53; }
+
+// RAII device grid pair.
+struct DeviceGrids {
+    void* a = nullptr;
+    void* b = nullptr;
+    ~DeviceGrids() {
+        if (a) stencil_free(a);
+        if (b) stencil_free(b);
+    }
+};
+
+}  // namespace
+
+double Stencil::cells() const {
+    return double(options.extent_x()) * double(options.extent_y()) * double(options.extent_z());
+}
+
+template <class T>
+void Stencil::init_typed(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) const {
+    // stencil.cpp:190-207: two zero-initialised buffers, x-ghost faces = 1.
+    matrix = BoundaryGrid<T>(options.dims, options.extent_x(), options.extent_y(), options.extent_z(), options.radius);
+    result = BoundaryGrid<T>(options.dims, options.extent_x(), options.extent_y(), options.extent_z(), options.radius);
+    matrix.fill_x_boundaries(T(1));
+    result.fill_x_boundaries(T(1));
+    if (options.random_init) {
+        // Extension: interior = splitmix64(seed + linear index) in [0,1),
+        // identical to stencil_fill_initial(STENCIL_INIT_RANDOM).
+        for (int64_t z = 0; z < matrix.depth(); ++z)
+            for (int64_t y = 0; y < matrix.height(); ++y)
+                for (int64_t x = 0; x < matrix.width(); ++x) {
+                    const uint64_t lin = (uint64_t(z) * uint64_t(matrix.height()) + uint64_t(y)) * uint64_t(matrix.width()) + uint64_t(x);
+                    T v;
+                    u01(splitmix64(options.seed + lin), v);
+                    matrix.elem_at(z, y, x) = v;
+                    result.elem_at(z, y, x) = v;
+                }
+    }
+}
+
+void Stencil::initialize_matrix() {
+    if (options.fp64) init_typed(matrix64, result64);
+    else init_typed(matrix32, result32);
+}
+
+template <class T>
+auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGrid<T>& result)
+    -> std::chrono::steady_clock::duration {
+    initialize_matrix();
+
+    stencil_problem p{};
+    p.dims = options.dims;
+    p.dtype = options.fp64 ? STENCIL_F64 : STENCIL_F32;
+    p.shape = options.box ? STENCIL_BOX : STENCIL_STAR;
+    p.radius = int(options.radius);
+    p.order = (method == DMA || method == RMA || method == DMA_SLAVE_PACK) ? STENCIL_ORDER_DMA : STENCIL_ORDER_NAIVE;
+    switch (method) {
+    case HIP_DIRECT: p.kernel = STENCIL_KERNEL_DIRECT; break;
+    case HIP_ZMARCH: p.kernel = STENCIL_KERNEL_ZMARCH; break;
+    case HIP_TEMPORAL2: p.kernel = STENCIL_KERNEL_TEMPORAL2; break;
+    case HIP: p.kernel = kernel_of(options.kernel); break;
+    default: p.kernel = STENCIL_KERNEL_AUTO; break;
+    }
+    p.nx = matrix.width();
+    p.ny = matrix.height();
+    p.nz = matrix.depth();
+
+    stencil_layout l;
+    check(stencil_layout_init(&p, &l), "stencil_layout_init");
+    check(stencil_set_device(options.device), "stencil_set_device");
+    DeviceGrids d;
+    check(stencil_alloc(&l, &d.a), "stencil_alloc");
+    check(stencil_alloc(&l, &d.b), "stencil_alloc");
+    check(stencil_upload(&l, d.a, matrix.data(), matrix.row_stride(), matrix.rows_with_boundary(), nullptr), "upload");
+    check(stencil_upload(&l, d.b, result.data(), result.row_stride(), result.rows_with_boundary(), nullptr), "upload");
+    check(stencil_synchronize(nullptr), "synchronize");
+
+    // Timed region, like stencil.cpp:33-54 (spawn ... join): the sweeps on
+    // grids already resident in device memory, until they have completed.
+    int final_in_b = 0;
+    float ms = 0.f;
+    auto const start = std::chrono::steady_clock::now();
+    check(stencil_iterate(&l, d.a, d.b, options.iterations, nullptr, &final_in_b, &ms), "stencil_iterate");
+    auto const end = std::chrono::steady_clock::now();
+    device_ms = ms;
+
+    // The final grid goes to the buffer the reference's parity rule names
+    // (stencil.cpp:88-92,134): `result` after an odd count, else `matrix`.
+    BoundaryGrid<T>& dst = (options.iterations & 1u) ? result : matrix;
+    check(stencil_download(&l, final_in_b ? d.b : d.a, dst.data(), dst.row_stride(), dst.rows_with_boundary(), nullptr), "download");
+    check(stencil_synchronize(nullptr), "synchronize");
+    return end - start;
+}
+
+auto Stencil::run(InputMethod method) -> std::chrono::steady_clock::duration {
+    return options.fp64 ? run_typed(method, matrix64, result64) : run_typed(method, matrix32, result32);
+}
+
+auto Stencil::run(std::string_view method_name) -> std::optional<std::chrono::steady_clock::duration> {
+    // Name -> method map (stencil.cpp:61-66) plus the GPU-native names.
+    static std::unordered_map<std::string_view, InputMethod> const method_map = {
+        {"DMA", DMA},
+        {"DMAStaticUnroll", DMA_STATIC_UNROLL},
+        {"DMASlavePack", DMA_SLAVE_PACK},
+        {"RMA", RMA},
+        {"HIP", HIP},
+        {"HIPDirect", HIP_DIRECT},
+        {"HIPZMarch", HIP_ZMARCH},
+        {"HIPTemporal2", HIP_TEMPORAL2},
+    };
+    auto const iter = method_map.find(method_name);
+    if (iter == method_map.end()) return std::nullopt;
+    return run(iter->second);
+}
+
+// The naive CPU sweep + comparison of stencil.cpp:75-151, generalised to the
+// engine's dims/shapes.  Naive order always (it is the reference's checker),
+// absolute tolerance 1e-4, first mismatch printed in the reference's format.
+template <class T>
+bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const {
+    BoundaryGrid<T> in, out;
+    init_typed(in, out);
+    const int r = int(options.radius);
+    const int64_t sx = in.row_stride(), sxy = sx * in.rows_with_boundary();
+    T avg;
+    if (options.box) {
+        int64_t w = 2 * r + 1, n = w * w * (options.dims == 3 ? w : 1);
+        avg = T(1) / T(n - 1);
+    } else {
+        avg = T(1) / T(2 * options.dims * r);  // stencil.cpp:85-86
+    }
+    bool swapped = false;
+    for (unsigned i = 0; i != options.iterations; ++i) {
+        T* src = in.data();
+        T* dst = out.data();
+        for (int64_t z = 0; z < in.depth(); ++z)
+            for (int64_t y = 0; y < in.height(); ++y)
+                for (int64_t x = 0; x < in.width(); ++x) {
+                    const int64_t zr = options.dims == 3 ? r : 0;
+                    const int64_t c = ((z + zr) * in.rows_with_boundary() + (y + r)) * sx + (x + r);
+                    T sum = T(0);
+                    if (options.box) {
+                        const int rz = options.dims == 3 ? r : 0;
+                        for (int dz = -rz; dz <= rz; ++dz)
+                            for (int dy = -r; dy <= r; ++dy)
+                                for (int dx = -r; dx <= r; ++dx)
+                                    if (dz || dy || dx) sum += src[c + dz * sxy + dy * sx + dx];
+                    } else {
+                        for (int k = r; k >= 1; --k) sum += src[c - k];       // left
+                        for (int k = 1; k <= r; ++k) sum += src[c + k];       // right
+                        for (int k = r; k >= 1; --k) sum += src[c - k * sx];  // top
+                        for (int k = 1; k <= r; ++k) sum += src[c + k * sx];  // bottom
+                        if (options.dims == 3) {
+                            for (int k = r; k >= 1; --k) sum += src[c - k * sxy];
+                            for (int k = 1; k <= r; ++k) sum += src[c + k * sxy];
+                        }
+                    }
+                    dst[c] = sum * avg;
+                }
+        std::swap(in, out);
+        swapped = !swapped;
+    }
+    const BoundaryGrid<T>& compared = swapped ? result : matrix;
+    for (int64_t z = 0; z < in.depth(); ++z)
+        for (int64_t y = 0; y < in.height(); ++y)
+            for (int64_t x = 0; x < in.width(); ++x) {
+                const double a = double(in.elem_at(z, y, x)), b = double(compared.elem_at(z, y, x));
+                if (std::fabs(a - b) >= 1e-4 || std::isnan(b)) {
+                    if (options.dims == 3)
+                        std::printf("invalid result at (%u, %u, %u): %.15f vs %.15f\n", unsigned(z), unsigned(y),
+                                    unsigned(x), a, b);
+                    else
+                        std::printf("invalid result at (%u, %u): %.15f vs %.15f\n", unsigned(y), unsigned(x), a, b);
+                    return false;
+                }
+            }
+    return true;
+}
+
+auto Stencil::check_result() const -> bool {
+    return options.fp64 ? check_typed(matrix64, result64) : check_typed(matrix32, result32);
+}

@@ -1,0 +1,162 @@
+"""Device-resident Jacobi engine: torch owns HBM and streams, every sweep is a
+HIP kernel launched through the C-ABI (stencil_amd/_lib.py).
+
+This is the Python counterpart of the C++ host engine (csrc/host/stencil.cpp,
+itself the mirror of the reference's class Stencil, src/stencil/stencil.cpp).
+It exposes what the benchmark, the tests and the multi-GPU slab driver need:
+two ping-pong grids in the engine's padded layout, the reference initial
+condition, single sweeps over slow-axis ranges, the whole-job iterate, and
+views of whole planes for halo exchange.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_TORCH_DTYPE = {_lib.F32: torch.float32, _lib.F64: torch.float64}
+_NP_DTYPE = {_lib.F32: np.float32, _lib.F64: np.float64}
+
+
+@dataclass(frozen=True)
+class StencilSpec:
+    dims: int = 3
+    dtype: str = "fp64"          # "fp32" | "fp64"
+    shape: str = "star"          # "star" | "box"
+    radius: int = 1
+    order: str = "naive"         # "naive" | "dma"
+    kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2"
+
+    def problem(self, nx: int, ny: int, nz: int) -> _lib.Problem:
+        return _lib.make_problem(
+            dims=self.dims, dtype=_lib.F64 if self.dtype == "fp64" else _lib.F32,
+            shape=_lib.BOX if self.shape == "box" else _lib.STAR, radius=self.radius,
+            order=_lib.ORDER_DMA if self.order == "dma" else _lib.ORDER_NAIVE,
+            kernel=_lib.KERNEL_NAMES[self.kernel], nx=nx, ny=ny, nz=nz if self.dims == 3 else 1)
+
+    @property
+    def elem_bytes(self) -> int:
+        return 8 if self.dtype == "fp64" else 4
+
+
+def _stream_handle(stream) -> ctypes.c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+class JacobiEngine:
+    """Two grids (a, b) of one problem on one GPU."""
+
+    def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int = 1, device: int | torch.device = 0,
+                 allocate: bool = True):
+        self.lib = _lib.load()
+        self.spec = spec
+        self.prob = spec.problem(nx, ny, nz)
+        self.layout = _lib.make_layout(self.prob)
+        self.device = torch.device("cuda", device) if isinstance(device, int) else device
+        self.torch_dtype = _TORCH_DTYPE[self.prob.dtype]
+        self.r = spec.radius
+        self.slow_extent = int(self.lib.stencil_slow_extent(ctypes.byref(self.layout)))
+        # one slow-axis unit = a whole plane (3D) or a whole padded row (2D)
+        self.unit = int(self.layout.plane if spec.dims == 3 else self.layout.row)
+        if allocate:
+            n = int(self.layout.elems) + 256 // spec.elem_bytes  # tail pad, as stencil_alloc
+            self.a = torch.empty(n, dtype=self.torch_dtype, device=self.device)
+            self.b = torch.empty(n, dtype=self.torch_dtype, device=self.device)
+
+    # ------------------------------------------------------------------ init
+    def fill_initial(self, grid: torch.Tensor, kind: str = "reference", seed: int = 0, stream=None) -> None:
+        k = _lib.INIT_RANDOM if kind == "random" else _lib.INIT_REFERENCE
+        _lib.check(self.lib.stencil_fill_initial(ctypes.byref(self.layout), ctypes.c_void_p(grid.data_ptr()), k,
+                                                 ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), _stream_handle(stream)),
+                   "stencil_fill_initial")
+
+    def reset(self, kind: str = "reference", seed: int = 0) -> None:
+        self.fill_initial(self.a, kind, seed)
+        self.fill_initial(self.b, kind, seed)
+
+    # ---------------------------------------------------------------- sweeps
+    def sweep(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, stream=None) -> None:
+        _lib.check(self.lib.stencil_sweep(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
+                                          ctypes.c_void_p(dst.data_ptr()), begin, end, _stream_handle(stream)),
+                   "stencil_sweep")
+
+    def sweep2(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, stream=None) -> None:
+        _lib.check(self.lib.stencil_sweep2(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
+                                           ctypes.c_void_p(dst.data_ptr()), begin, end, _stream_handle(stream)),
+                   "stencil_sweep2")
+
+    def iterate(self, iterations: int, stream=None, timed: bool = False):
+        """Whole job a -> ... ; returns (final grid tensor, device ms or None)."""
+        fin = ctypes.c_int(0)
+        ms = ctypes.c_float(0.0)
+        _lib.check(self.lib.stencil_iterate(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
+                                            ctypes.c_void_p(self.b.data_ptr()), iterations, _stream_handle(stream),
+                                            ctypes.byref(fin), ctypes.byref(ms) if timed else None),
+                   "stencil_iterate")
+        return (self.b if fin.value else self.a), (ms.value if timed else None)
+
+    def plan(self, iterations: int):
+        launches = ctypes.c_int64(0)
+        kernel = ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_plan(ctypes.byref(self.layout), iterations, ctypes.byref(launches),
+                                         ctypes.byref(kernel)), "stencil_plan")
+        return int(launches.value), int(kernel.value)
+
+    # ----------------------------------------------------------------- views
+    def plane_view(self, grid: torch.Tensor, first: int, count: int) -> torch.Tensor:
+        """Contiguous 1-D view of slow-axis units [first, first+count), ghost
+        units included (first may be -r .. n+r-count)."""
+        r = self.r
+        if self.spec.dims == 3:
+            base = r * int(self.layout.plane)
+        else:
+            base = int(self.layout.origin) - int(self.layout.origin) % int(self.layout.row)
+        start = base + first * self.unit
+        return grid[start:start + count * self.unit]
+
+    def interior(self, grid: torch.Tensor) -> torch.Tensor:
+        """Strided (nz, ny, nx) / (ny, nx) view of the interior."""
+        p, lay = self.prob, self.layout
+        if self.spec.dims == 3:
+            return grid.as_strided((p.nz, p.ny, p.nx), (lay.plane, lay.row, 1), lay.origin)
+        return grid.as_strided((p.ny, p.nx), (lay.row, 1), lay.origin)
+
+    def with_ghosts(self, grid: torch.Tensor) -> torch.Tensor:
+        """Strided view of interior + ghost ring, the oracle's dense shape."""
+        p, lay, r = self.prob, self.layout, self.r
+        corner = lay.origin - r * lay.row - r - (r * lay.plane if self.spec.dims == 3 else 0)
+        if self.spec.dims == 3:
+            return grid.as_strided((p.nz + 2 * r, p.ny + 2 * r, p.nx + 2 * r), (lay.plane, lay.row, 1), corner)
+        return grid.as_strided((p.ny + 2 * r, p.nx + 2 * r), (lay.row, 1), corner)
+
+    def to_numpy(self, grid: torch.Tensor) -> np.ndarray:
+        """Dense host copy with ghosts (oracle layout)."""
+        torch.cuda.synchronize(self.device)
+        return self.with_ghosts(grid).cpu().numpy().copy()
+
+    def plane_sums(self, grid: torch.Tensor, stream=None) -> np.ndarray:
+        out = np.zeros(self.slow_extent, dtype=np.float64)
+        _lib.check(self.lib.stencil_plane_sums(ctypes.byref(self.layout), ctypes.c_void_p(grid.data_ptr()),
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                               _stream_handle(stream)), "stencil_plane_sums")
+        return out
+
+
+def copy_bandwidth(nbytes: int, reps: int = 20, device: int = 0) -> float:
+    """Attainable HBM bandwidth (GB/s, read+write) of a plain float4 copy."""
+    lib = _lib.load()
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device))
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    ms = ctypes.c_float(0.0)
+    _lib.check(lib.stencil_copy_bandwidth(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                          nbytes, 2, _stream_handle(None), ctypes.byref(ms)), "copy warmup")
+    _lib.check(lib.stencil_copy_bandwidth(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                          nbytes, reps, _stream_handle(None), ctypes.byref(ms)), "copy")
+    return 2.0 * nbytes * reps / (ms.value * 1e-3) / 1e9

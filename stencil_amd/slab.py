@@ -1,0 +1,172 @@
+"""Z-slab decomposition of the Jacobi sweep across processes (one per GPU).
+
+The reference decomposes its grid into an 8x8 mesh of CPE blocks and
+exchanges 4 halo strips per iteration by DMA through main memory or by RMA
+into the neighbour's LDM (src/stencil/slave/stencil_dma.cpp:236-247,
+stencil_rma.cpp:198-255), with a 64-core barrier per iteration
+(stencil_dma.cpp:562-563).  Across GPUs the natural cut is contiguous slabs of
+the slow axis (z in 3D, y in 2D): each rank owns planes [z0, z0 + n) plus r
+ghost planes per side, and one iteration exchanges r whole, contiguous planes
+with rank-1 and rank+1 -- no packing, and on an 8-GPU MI355X node every
+neighbour pair has its own xGMI link.
+
+Per iteration, on each rank (overlap=True):
+  stream A: sweep the 2r boundary planes -> post send/recv of them to the
+            neighbours (torch.distributed P2P; RCCL on GPUs, gloo on CPUs);
+  stream B: sweep the interior planes meanwhile;
+  join:     the next sweep waits for both streams and the received halos.
+Every cell's arithmetic is the single-GPU kernel's, so results are bitwise
+identical for any number of ranks (tests/test_slab_gloo.py, tests/test_gpu_*).
+
+`backend` is the per-rank compute object: stencil_amd.engine.JacobiEngine on
+a GPU.  The driver only needs sweep(), plane_view(), fill_initial() and the
+two grids a/b from it, so the CPU tests drive the identical exchange logic
+with the oracle as a stand-in backend.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def partition(n: int, world: int, rank: int) -> tuple[int, int]:
+    """(first, count) of rank's contiguous share of n planes; the remainder
+    goes to the lowest ranks."""
+    base, rem = divmod(n, world)
+    count = base + (1 if rank < rem else 0)
+    first = rank * base + min(rank, rem)
+    return first, count
+
+
+class TorchDistExchanger:
+    """Halo exchange with the slab neighbours over torch.distributed P2P."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        self.rank, self.world, self.group = rank, world, group
+
+    def exchange(self, send_lo, send_hi, recv_lo, recv_hi):
+        ops = []
+        if self.rank > 0:
+            ops.append(dist.P2POp(dist.isend, send_lo, self.rank - 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, recv_lo, self.rank - 1, self.group))
+        if self.rank < self.world - 1:
+            ops.append(dist.P2POp(dist.isend, send_hi, self.rank + 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, recv_hi, self.rank + 1, self.group))
+        if not ops:
+            return []
+        return dist.batch_isend_irecv(ops)
+
+
+@dataclass
+class SlabInfo:
+    rank: int
+    world: int
+    first: int   # global index of the first owned plane
+    count: int   # owned planes
+
+
+class SlabJacobi:
+    """One rank's share of a slab-decomposed Jacobi job."""
+
+    def __init__(self, backend, slab: SlabInfo, exchanger, overlap: bool = True):
+        self.be = backend
+        self.slab = slab
+        self.ex = exchanger
+        self.overlap = overlap
+        self.r = backend.r
+        n = slab.count
+        if slab.world > 1 and n < self.r:
+            raise ValueError(f"rank {slab.rank} owns {n} planes < radius {self.r}; use fewer ranks")
+        self.cur, self.nxt = backend.a, backend.b
+        self.on_gpu = self.cur.device.type == "cuda"
+        self._timing = None  # list of (start, end) events around interior sweeps
+        if self.on_gpu:
+            self.stream_bnd = torch.cuda.Stream(device=self.cur.device, priority=-1)  # high priority
+            self.stream_int = torch.cuda.Stream(device=self.cur.device)
+
+    # -------------------------------------------------------------- helpers
+    def _halo_views(self, grid):
+        n, r, be = self.slab.count, self.r, self.be
+        return (be.plane_view(grid, 0, r), be.plane_view(grid, n - r, r),
+                be.plane_view(grid, -r, r), be.plane_view(grid, n, r))
+
+    def init(self, kind: str = "reference", seed: int = 0, plane_elems: int = 0) -> None:
+        """Initial condition of the global grid restricted to this slab.
+        `plane_elems` = interior cells per slow-axis unit, so the random
+        interior uses global linear indices (seed shifted by first*plane)."""
+        s = seed + self.slab.first * plane_elems
+        self.be.fill_initial(self.be.a, kind, s)
+        self.be.fill_initial(self.be.b, kind, s)
+        self.cur, self.nxt = self.be.a, self.be.b
+        self._exchange_blocking(self.cur)
+
+    def _exchange_blocking(self, grid) -> None:
+        if self.slab.world == 1:
+            return
+        if self.on_gpu:
+            torch.cuda.current_stream().synchronize()
+        for w in self.ex.exchange(*self._halo_views(grid)):
+            w.wait()
+        if self.on_gpu:
+            torch.cuda.current_stream().synchronize()
+
+    # ----------------------------------------------------------------- step
+    def step(self) -> None:
+        src, dst = self.cur, self.nxt
+        n, r = self.slab.count, self.r
+        if self.slab.world == 1:
+            self.be.sweep(src, dst, 0, n)
+        elif not self.overlap or n <= 2 * r:
+            self.be.sweep(src, dst, 0, n)
+            for w in self.ex.exchange(*self._halo_views(dst)):
+                w.wait()
+        elif not self.on_gpu:
+            self.be.sweep(src, dst, 0, r)
+            self.be.sweep(src, dst, n - r, n)
+            works = self.ex.exchange(*self._halo_views(dst))
+            self.be.sweep(src, dst, r, n - r)
+            for w in works:
+                w.wait()
+        else:
+            main = torch.cuda.current_stream()
+            sa, sb = self.stream_bnd, self.stream_int
+            sa.wait_stream(main)
+            sb.wait_stream(main)
+            with torch.cuda.stream(sa):
+                self.be.sweep(src, dst, 0, r, stream=sa)
+                self.be.sweep(src, dst, n - r, n, stream=sa)
+                works = self.ex.exchange(*self._halo_views(dst))
+            with torch.cuda.stream(sb):
+                if self._timing is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(sb)
+                self.be.sweep(src, dst, r, n - r, stream=sb)
+                if self._timing is not None:
+                    ev1.record(sb)
+                    self._timing.append((ev0, ev1))
+            for w in works:
+                w.wait()  # current (main) stream waits for the P2P
+            main.wait_stream(sa)
+            main.wait_stream(sb)
+        self.cur, self.nxt = dst, src
+
+    # ------------------------------------------------------- kernel timing
+    def start_kernel_timing(self) -> None:
+        """Record HIP events on the interior stream around every interior
+        sweep (the dominant kernel) until stop_kernel_timing()."""
+        self._timing = []
+
+    def stop_kernel_timing(self) -> tuple[float, int]:
+        """(total ms of the recorded interior sweeps, number of launches)."""
+        ev, self._timing = self._timing or [], None
+        if not ev:
+            return 0.0, 0
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev), len(ev)
+
+    def run(self, iterations: int) -> None:
+        for _ in range(iterations):
+            self.step()

@@ -1,0 +1,101 @@
+"""The C-ABI library loads, exports every symbol include/stencil_hip.h
+declares, keeps the reference's struct layouts, and validates problems --
+all without touching a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from stencil_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "stencil_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?\w+\s*\**\s*(stencil_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_what_binding_knows():
+    decl = declared_functions()
+    assert len(decl) >= 20
+    assert set(decl) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_library_has_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_reference_struct_layouts():
+    # struct Arguments is 88 bytes on LP64; each
+    # BoundaryMatrixView<float> is 40 bytes.
+    assert ctypes.sizeof(_lib.MatrixView) == 40
+    assert ctypes.sizeof(_lib.Arguments) == 88
+    assert _lib.Arguments.input.offset == 8 and _lib.Arguments.output.offset == 48
+    assert ctypes.sizeof(_lib.Problem) == 48
+
+
+@pytest.mark.parametrize("dims,dtype,r,n", [(2, _lib.F32, 1, (1024, 1024, 1)), (3, _lib.F64, 1, (512, 512, 512)),
+                                            (3, _lib.F32, 2, (70, 19, 6)), (2, _lib.F64, 40, (5, 3, 1))])
+def test_layout_alignment(dims, dtype, r, n):
+    lay = _lib.make_layout(_lib.make_problem(dims=dims, dtype=dtype, radius=r, nx=n[0], ny=n[1], nz=n[2]))
+    es = 8 if dtype == _lib.F64 else 4
+    align = 128 // es
+    ox = lay.origin % lay.row
+    assert ox % align == 0 and ox >= r                      # interior x=0 is 128-B aligned, ghosts fit
+    assert lay.row % align == 0 and lay.row >= ox + n[0] + r
+    assert lay.rows == n[1] + 2 * r
+    assert lay.plane == lay.row * lay.rows
+    assert lay.planes == (n[2] + 2 * r if dims == 3 else 1)
+    assert lay.bytes == lay.elems * es == lay.plane * lay.planes * es
+    lib = _lib.load()
+    assert lib.stencil_slow_extent(ctypes.byref(lay)) == (n[2] if dims == 3 else n[1])
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(dims=4), _lib.STENCIL_OK - 1),
+    (dict(radius=0), -1),
+    (dict(dims=3, order=_lib.ORDER_DMA), -1),
+    (dict(dims=2, shape=_lib.BOX, order=_lib.ORDER_DMA), -1),
+    (dict(nx=-3), -1),
+    (dict(dims=2, nz=5), -1),
+    (dict(dims=2, nz=1, kernel=_lib.KERNEL_ZMARCH), -5),
+    (dict(dims=3, shape=_lib.BOX, kernel=_lib.KERNEL_ZMARCH), -5),
+])
+def test_layout_rejects_invalid(kw, code):
+    base = dict(dims=3, dtype=_lib.F64, nx=8, ny=8, nz=8)
+    base.update(kw)
+    prob = _lib.Problem(base.get("dims"), base.get("dtype"), base.get("shape", 0), base.get("radius", 1),
+                        base.get("order", 0), base.get("kernel", 0), base.get("nx"), base.get("ny"), base.get("nz"))
+    lib = _lib.load()
+    lay = _lib.Layout()
+    rc = lib.stencil_layout_init(ctypes.byref(prob), ctypes.byref(lay))
+    assert rc == code
+    assert lib.stencil_last_error_message()
+
+
+def test_error_strings():
+    lib = _lib.load()
+    for code in (0, -1, -2, -3, -4, -5, -99):
+        assert lib.stencil_strerror(code)
+    with pytest.raises(_lib.StencilError):
+        _lib.make_layout(_lib.make_problem(dims=2, radius=0, nx=4, ny=4))
+
+
+def test_plan_counts_launches():
+    lib = _lib.load()
+    lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
+    launches, kernel = ctypes.c_int64(), ctypes.c_int32()
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 7 and kernel.value == _lib.KERNEL_ZMARCH

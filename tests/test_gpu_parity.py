@@ -1,0 +1,182 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the CPU oracle.
+
+Bit-exact everywhere: every kernel performs the reference's additions and
+multiply in the reference's order (naive = check_result, stencil.cpp:104-125;
+dma = stencil_dma.cpp:431-444 / 636-650), compiled without FMA contraction and
+without denormal flushing.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def engine(gpu, dims, dtype, shape, r, order, kernel, nx, ny, nz):
+    from stencil_amd.engine import JacobiEngine, StencilSpec
+    return JacobiEngine(StencilSpec(dims=dims, dtype=dtype, shape=shape, radius=r, order=order, kernel=kernel),
+                        nx, ny, nz, device=gpu)
+
+
+def gpu_run(gpu, dims, dtype, shape, r, order, kernel, nx, ny, nz, it, init="reference", seed=0):
+    e = engine(gpu, dims, dtype, shape, r, order, kernel, nx, ny, nz)
+    e.reset(init, seed)
+    fin, _ = e.iterate(it)
+    return e, e.to_numpy(fin)
+
+
+def same_bits(a, b):
+    return a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+# ---------------------------------------------------------------- fixtures
+def _fixture_cases():
+    fx = np.load(os.path.join(GOLD, "oracle_fixtures.npz"))
+    return [k for k in fx.files if not k.endswith("__meta")]
+
+
+@pytest.mark.parametrize("name", _fixture_cases())
+@pytest.mark.parametrize("kernel", ["direct", "auto"])
+def test_golden_fixtures(gpu, name, kernel):
+    fx = np.load(os.path.join(GOLD, "oracle_fixtures.npz"))
+    dims, f64, box, r, dma, nx, ny, nz, it, rnd, seed = (int(x) for x in fx[name + "__meta"])
+    e, g = gpu_run(gpu, dims, "fp64" if f64 else "fp32", "box" if box else "star", r, "dma" if dma else "naive",
+                   kernel, nx, ny, nz, it, "random" if rnd else "reference", seed)
+    p = ob.problem(dims, "fp64" if f64 else "fp32", "box" if box else "star", r, "dma" if dma else "naive", nx, ny, nz)
+    assert same_bits(np.ascontiguousarray(ob.interior(p, g)), fx[name])
+
+
+# ------------------------------------------------ reference configs (2D)
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("order", ["naive", "dma"])
+def test_c1_1024_100_iterations(gpu, dtype, order):
+    """BASELINE config 1 (2D 5-point, 1024^2, 100 iterations)."""
+    p = ob.problem(2, dtype, "star", 1, order, 1024, 1024)
+    want = ob.run(p, 100, threads=8)
+    _, got = gpu_run(gpu, 2, dtype, "star", 1, order, "auto", 1024, 1024, 1, 100)
+    assert same_bits(got, want)
+    if order == "naive":
+        sums = {"fp32": 10520.714292108827, "fp64": 10520.714308906061}
+        assert ob.interior_sum(p, got) == pytest.approx(sums[dtype], rel=1e-15, abs=0)
+
+
+@pytest.mark.parametrize("r", [1, 2, 3, 5])
+@pytest.mark.parametrize("order", ["naive", "dma"])
+def test_2d_radius_random(gpu, r, order):
+    p = ob.problem(2, "fp32", "star", r, order, 131, 77)
+    want = ob.run(p, 9, "random", 42)
+    _, got = gpu_run(gpu, 2, "fp32", "star", r, order, "auto", 131, 77, 1, 9, "random", 42)
+    assert same_bits(got, want)
+
+
+# ------------------------------------------------------- 3D hot kernels
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("kernel", ["direct", "zmarch"])
+@pytest.mark.parametrize("shape3", [(64, 16, 8), (130, 37, 29), (1, 1, 1), (65, 17, 3), (200, 3, 70)])
+def test_3d_7pt_random_ragged(gpu, dtype, kernel, shape3):
+    nx, ny, nz = shape3
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    for it in (1, 2, 5):
+        want = ob.run(p, it, "random", 1234 + it)
+        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", kernel, nx, ny, nz, it, "random", 1234 + it)
+        assert same_bits(got, want), (it, shape3)
+
+
+@pytest.mark.parametrize("shape,r", [("box", 1), ("star", 2), ("star", 3), ("box", 2)])
+def test_3d_other_shapes(gpu, shape, r):
+    p = ob.problem(3, "fp64", shape, r, "naive", 45, 23, 17)
+    want = ob.run(p, 3, "random", 5)
+    _, got = gpu_run(gpu, 3, "fp64", shape, r, "naive", "auto", 45, 23, 17, 3, "random", 5)
+    assert same_bits(got, want)
+
+
+def test_zero_iterations_and_empty(gpu):
+    p = ob.problem(3, "fp64", "star", 1, "naive", 20, 10, 5)
+    _, got = gpu_run(gpu, 3, "fp64", "star", 1, "naive", "auto", 20, 10, 5, 0, "random", 9)
+    assert same_bits(got, ob.init(p, "random", 9))
+    e = engine(gpu, 3, "fp64", "star", 1, "naive", "auto", 0, 4, 4)
+    e.reset()
+    e.iterate(3)  # empty interior: nothing to do, must not fault
+
+
+def test_full_size_c2_bitwise_few_iterations(gpu):
+    """BASELINE config 2 size (512^3 fp64 7-point) at full size: bitwise
+    against the oracle for 3 sweeps (the oracle's multithreaded run takes a
+    few seconds), and the two kernel families bitwise against each other."""
+    n = 512
+    p = ob.problem(3, "fp64", "star", 1, "naive", n, n, n)
+    want = ob.run(p, 3, "random", 77, threads=16)
+    _, got = gpu_run(gpu, 3, "fp64", "star", 1, "naive", "auto", n, n, n, 3, "random", 77)
+    assert same_bits(got, want)
+
+
+def test_full_size_c2_1000_iterations_properties(gpu):
+    """The whole config-2 job (1000 sweeps, reference initial condition):
+    ghost cells untouched, bitwise x-mirror symmetry (0+L+R == 0+R+L), all
+    values in [0, 1], plane checksums identical across kernel families."""
+    import torch
+    n = 512
+    e = engine(gpu, 3, "fp64", "star", 1, "naive", "zmarch", n, n, n)
+    e.reset()
+    init = e.with_ghosts(e.a).clone()
+    fin, _ = e.iterate(1000)
+    g = e.with_ghosts(fin)
+    inner = e.interior(fin)
+    assert torch.equal(inner, torch.flip(inner, dims=[2]))
+    assert float(inner.min()) >= 0.0 and float(inner.max()) <= 1.0
+    mask = torch.ones_like(g, dtype=torch.bool)
+    mask[1:-1, 1:-1, 1:-1] = False
+    assert torch.equal(g[mask], init[mask])
+    sums_zm = e.plane_sums(fin)
+    e2 = engine(gpu, 3, "fp64", "star", 1, "naive", "direct", n, n, n)
+    e2.reset()
+    fin2, _ = e2.iterate(1000)
+    assert np.array_equal(sums_zm, e2.plane_sums(fin2))
+    assert torch.equal(e2.interior(fin2), inner)
+
+
+# ------------------------------------------- reference-compatible entry points
+@pytest.mark.parametrize("fn,order", [("stencil_iterate_dma", "dma"), ("stencil_iterate_dma_static_unroll", "naive"),
+                                      ("stencil_iterate_dma_slave_pack", "dma"), ("stencil_iterate_rma", "dma")])
+@pytest.mark.parametrize("n,it,r", [(64, 100, 1), (64, 7, 1), (96, 50, 3), (32, 0, 1)])
+def test_reference_abi_entry_points(gpu, fn, order, n, it, r):
+    """stencil_iterate_*(Arguments*) with host buffers: the final grid must
+    land in `output` when iterations is odd, else in `input`
+    (stencil.cpp:88-92,134), equal bit for bit to that variant's order."""
+    from stencil_amd import _lib
+    lib = _lib.load()
+    p = ob.problem(2, "fp32", "star", r, order, n, n)
+    a = ob.init(p)
+    b = a.copy()
+    def view(arr):
+        return _lib.MatrixView(n + 2 * r, n + 2 * r, r, r, n + 2 * r, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    args = _lib.Arguments(n // 8 or 1, it, view(a), view(b))
+    getattr(lib, fn)(ctypes.byref(args))
+    assert lib.stencil_last_error() == 0, lib.stencil_last_error_message()
+    got = b if it % 2 else a
+    assert same_bits(got, ob.run(p, it))
+
+
+# ----------------------------------------------------------------- CLI
+def test_cli_check_result_on_gpu(gpu):
+    cli = os.path.join(ROOT, "build", "bin", "stencil_main")
+    out = subprocess.run([cli, "-s", "64", "-b", "8", "-i", "100", "-m", "DMA", "DMAStaticUnroll", "DMASlavePack",
+                          "RMA", "HIP", "-c", "-R", "2"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    import re
+    for m in ("DMA", "DMAStaticUnroll", "DMASlavePack", "RMA", "HIP"):
+        assert f"The results of method {m} is correct." in out.stdout
+        assert re.search(rf"The average time taken by {m} method is [0-9.e+-]+ms for 100 iterations\.", out.stdout)
+    out = subprocess.run([cli, "-s", "24", "-b", "1", "-i", "5", "-m", "HIP", "HIPDirect", "HIPZMarch", "-c",
+                          "--points", "7", "--dtype", "fp64", "--init", "random"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr + out.stdout
+    assert out.stdout.count("is correct.") == 3

@@ -1,0 +1,95 @@
+"""Pin the CPU oracle (oracle/) against the reference's known answers
+(tests/golden/survey_known_answers.json) and freeze it with
+the committed fixtures (tests/golden/oracle_fixtures.npz)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+KA = json.load(open(os.path.join(GOLD, "survey_known_answers.json")))
+
+
+@pytest.mark.parametrize("case", KA["fp32_naive_sums"], ids=lambda c: f"n{c['n']}_i{c['iterations']}_r{c['radius']}")
+def test_fp32_naive_sum_matches_reference(case):
+    p = ob.problem(2, "fp32", radius=case["radius"], nx=case["n"], ny=case["n"])
+    g = ob.run(p, case["iterations"])
+    assert ob.interior_sum(p, g) == pytest.approx(case["sum"], rel=1e-15, abs=0)
+
+
+@pytest.mark.parametrize("case", KA["fp64_naive_sums"], ids=lambda c: f"n{c['n']}_i{c['iterations']}_r{c['radius']}")
+def test_fp64_naive_sum_matches_survey(case):
+    p = ob.problem(2, "fp64", radius=case["radius"], nx=case["n"], ny=case["n"])
+    g = ob.run(p, case["iterations"])
+    assert ob.interior_sum(p, g) == pytest.approx(case["sum"], rel=1e-15, abs=0)
+
+
+def test_c1_fp64_spot_values():
+    c = KA["c1_fp64_spot_values"]
+    p = ob.problem(2, "fp64", nx=c["n"], ny=c["n"])
+    inner = ob.interior(p, ob.run(p, c["iterations"]))
+    for v in c["values"]:
+        assert inner[v["row"], v["col"]] == v["value"]
+
+
+@pytest.mark.parametrize("case", KA["dma_vs_naive_fp32"], ids=lambda c: f"n{c['n']}_r{c['radius']}")
+def test_dma_order_deviation_matches_reference(case):
+    """The reference DMA kernel differs from the naive loop by a recorded
+    amount; the restated DMA order must reproduce it."""
+    n, it, r = case["n"], case["iterations"], case["radius"]
+    a = ob.interior(ob.problem(2, "fp32", radius=r, nx=n, ny=n), ob.run(ob.problem(2, "fp32", radius=r, nx=n, ny=n), it))
+    pd = ob.problem(2, "fp32", radius=r, order="dma", nx=n, ny=n)
+    b = ob.interior(pd, ob.run(pd, it))
+    d = np.abs(a.astype(np.float64) - b)
+    rel = (d / np.maximum(np.abs(a), 1e-30)).max()
+    assert d.max() <= case["max_abs_le"]
+    assert abs(rel - case["max_rel"]) <= case["rel_tol"]
+
+
+def test_dma_equals_naive_small():
+    for c in KA["dma_equals_naive"]:
+        pn = ob.problem(2, "fp32", nx=c["n"], ny=c["n"])
+        pd = ob.problem(2, "fp32", order="dma", nx=c["n"], ny=c["n"])
+        assert np.array_equal(ob.run(pn, c["iterations"]), ob.run(pd, c["iterations"]))
+
+
+def test_fixtures_reproduce_bitwise():
+    fx = np.load(os.path.join(GOLD, "oracle_fixtures.npz"))
+    names = [k for k in fx.files if not k.endswith("__meta")]
+    assert len(names) >= 8
+    for name in names:
+        m = fx[name + "__meta"]
+        dims, f64, box, r, dma, nx, ny, nz, it, rnd, seed = (int(x) for x in m)
+        p = ob.problem(dims, "fp64" if f64 else "fp32", "box" if box else "star", r, "dma" if dma else "naive", nx, ny, nz)
+        g = ob.run(p, it, "random" if rnd else "reference", seed)
+        assert np.array_equal(ob.interior(p, g).view(np.uint8), fx[name].view(np.uint8)), name
+
+
+@pytest.mark.parametrize("dims,shape,r", [(2, "star", 1), (2, "star", 3), (3, "star", 1), (3, "box", 1), (3, "star", 2)])
+def test_ghosts_never_written_and_parity(dims, shape, r):
+    p = ob.problem(dims, "fp64", shape, r, "naive", 11, 9, 7)
+    a0 = ob.init(p, "random", 1)
+    for it in (0, 1, 2, 5):
+        g = ob.run(p, it, "random", 1)
+        mask = np.ones_like(g, dtype=bool)
+        mask[tuple(slice(r, -r) for _ in range(g.ndim))] = False
+        assert np.array_equal(g[mask], a0[mask])
+        if it == 0:
+            assert np.array_equal(g, a0)
+
+
+def test_threads_do_not_change_bits():
+    p = ob.problem(3, "fp64", "star", 1, "naive", 40, 33, 20)
+    assert np.array_equal(ob.run(p, 4, "random", 2, threads=1), ob.run(p, 4, "random", 2, threads=4))
+
+
+def test_x_mirror_symmetry_reference_init():
+    """x-ghost faces are both 1, and left/right are the first two addends
+    (0 + L + R == 0 + R + L exactly), so the reference solution is bitwise
+    symmetric under x -> nx-1-x."""
+    p = ob.problem(2, "fp32", nx=50, ny=31)
+    inner = ob.interior(p, ob.run(p, 40))
+    assert np.array_equal(inner, inner[:, ::-1])
