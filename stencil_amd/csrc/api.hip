@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -66,6 +67,15 @@ int sweep_family(const stencil_problem& p) {
     if (p.kernel == STENCIL_KERNEL_DIRECT) return STENCIL_KERNEL_DIRECT;
     if (zmarch_supports(p)) return STENCIL_KERNEL_ZMARCH;
     return STENCIL_KERNEL_DIRECT;
+}
+
+// Does stencil_iterate fuse pairs of sweeps?  Explicit TEMPORAL2, or AUTO on
+// a problem the fused kernel supports (STENCIL_NO_T2=1 disables the latter).
+bool iterate_fused(const stencil_problem& p) {
+    if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
+    if (p.kernel != STENCIL_KERNEL_AUTO || !temporal2_supports(p)) return false;
+    const char* e = std::getenv("STENCIL_NO_T2");
+    return !(e && *e && *e != '0');
 }
 
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
@@ -129,10 +139,19 @@ __global__ void __launch_bounds__(256) plane_sums_kernel(const T* __restrict__ b
     if (threadIdx.x == 0) out[s] = red[0];
 }
 
-__global__ void __launch_bounds__(256) copy_kernel(float4* __restrict__ dst, const float4* __restrict__ src,
+// Streaming copy used to calibrate attainable HBM bandwidth: 4 independent
+// 16-B loads in flight per lane, one pass, no grid-stride loop.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) copy_kernel(f32x4* __restrict__ dst, const f32x4* __restrict__ src,
                                                    int64_t n) {
-    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+    const int64_t base = int64_t(blockIdx.x) * 1024 + threadIdx.x;
+    f32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + k * 256 < n) v[k] = __builtin_nontemporal_load(src + base + k * 256);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + k * 256 < n) __builtin_nontemporal_store(v[k], dst + base + k * 256);
 }
 
 // Host pointer of the first allocated element of plane `p` (slow-axis
@@ -323,7 +342,7 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
 
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {
     if (int rc = check_layout(l)) return rc;
-    const bool t2 = l->prob.kernel == STENCIL_KERNEL_TEMPORAL2;
+    const bool t2 = iterate_fused(l->prob);
     if (launches) *launches = t2 ? int64_t(iterations / 2 + iterations % 2) : int64_t(iterations);
     if (kernel) *kernel = t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
     return STENCIL_OK;
@@ -341,7 +360,7 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         STENCIL_HIP_CHECK(hipEventRecord(e0, s));
     }
     const int64_t n = stencil_slow_extent(l);
-    const bool t2 = l->prob.kernel == STENCIL_KERNEL_TEMPORAL2;
+    const bool t2 = iterate_fused(l->prob);
     void* in = a;
     void* out = b;
     bool swapped = false;
@@ -405,11 +424,11 @@ int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, 
     STENCIL_HIP_CHECK(hipEventCreate(&e0));
     STENCIL_HIP_CHECK(hipEventCreate(&e1));
     const int64_t n = bytes / 16;
-    const unsigned blocks = unsigned(std::min<int64_t>((n + 255) / 256, 256 * 16));
+    const unsigned blocks = unsigned((n + 1023) / 1024);
     STENCIL_HIP_CHECK(hipEventRecord(e0, s));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, s, static_cast<float4*>(dst),
-                           static_cast<const float4*>(src), n);
+        hipLaunchKernelGGL(copy_kernel, dim3(blocks), dim3(256), 0, s, static_cast<f32x4*>(dst),
+                           static_cast<const f32x4*>(src), n);
     STENCIL_LAUNCH_CHECK();
     STENCIL_HIP_CHECK(hipEventRecord(e1, s));
     STENCIL_HIP_CHECK(hipEventSynchronize(e1));

@@ -1,12 +1,260 @@
-// kernels_temporal.hip -- fused two-step (temporal blocking) sweeps.
+// kernels_temporal.hip -- two fused Jacobi sweeps per launch (temporal
+// blocking) for the 3D 7-point star (r = 1, naive order).
+//
+// One launch reads grid t from HBM once and writes grid t+2 once; t+1 never
+// leaves the chip.  Per launch: ~1.2 x 8 B read + 8 B written per cell for TWO
+// updates, against 2 x 16 B for two plain sweeps.
+//
+// Geometry (a workgroup = NW waves; V = 16 B / sizeof(T) elements per lane):
+//   * the workgroup's lanes cover an input REGION of 64*V x NW*RY cells of
+//     each plane: the output tile (TX = 64V - 2V by TY = NW*RY - 4) plus a
+//     2-cell ring (x: one V-vector per side, keeping 16-B alignment);
+//   * it marches z over a chunk of output planes [za, zb).  Iteration p:
+//        LDS_in  <- in(p-1)                       (double-buffered)
+//        barrier
+//        t1(p-1) =  S(in) on the region minus its outer ring, or in(p-1)
+//                   where the cell is a ghost (Dirichlet: ghosts never change)
+//        LDS_t1  <- t1(p-1)                       (double-buffered)
+//        t2(p-2) =  S(t1) on the output tile, x/y neighbours of t1(p-2) from
+//                   LDS (written last iteration), z neighbours t1(p-3),
+//                   t1(p-1) from registers  -> store
+//     one barrier per plane; in(p-2..p+1) and t1(p-3..p-1) live in 4-slot
+//     register rings (plane p+2 is prefetched as soon as in(p-2) is dead).
+//   * XCD-aware tile numbering as in kernels_zmarch.hip.
+//
+// Every cell of t1 and t2 is computed with exactly the single-sweep order
+// (x-, x+, y-, y+, z-, z+, from 0, then * avg), so two fused steps are
+// bitwise equal to two plain sweeps (tests/test_gpu_parity.py).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace stencil {
+namespace {
 
-bool temporal2_supports(const stencil_problem&) { return false; }
+template <typename T, int V>
+struct Vec {
+    typedef T type __attribute__((ext_vector_type(V)));
+};
 
-int launch_temporal2(const stencil_layout&, const void*, void*, int64_t, int64_t, hipStream_t) {
-    return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 not built");
+template <typename T, int V, int RY, int NW>
+struct T2Tile {
+    static constexpr int RW = 64 * V;      // region width
+    static constexpr int TX = RW - 2 * V;  // output tile width
+    static constexpr int RH = NW * RY;     // region height
+    static constexpr int TY = RH - 4;      // output tile height
+    static constexpr int LX = RW + 2 * V;  // LDS row: pad V | region RW | pad V
+    static constexpr int LY = RH + 2;      // LDS rows: pad | region RH | pad
+};
+
+template <typename T, int V, int RY, int NW>
+__global__ void __launch_bounds__(64 * NW)
+    temporal2_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
+                  int zchunk, int tiles_x, int tiles_y, int tiles_z, T avg) {
+    using Tl = T2Tile<T, V, RY, NW>;
+    using VT = typename Vec<T, V>::type;
+    constexpr int TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
+    __shared__ __attribute__((aligned(16))) T lin[2][LY][LX];
+    __shared__ __attribute__((aligned(16))) T lt1[2][LY][LX];
+
+    // ---- XCD-aware tile order (speed only) ----
+    const int nb = tiles_x * tiles_y * tiles_z;
+    int t = blockIdx.x;
+    if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
+    const int bx = t % tiles_x;
+    const int by = (t / tiles_x) % tiles_y;
+    const int bz = t / (tiles_x * tiles_y);
+
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x0 = int64_t(bx) * TX, y0 = int64_t(by) * TY;
+    const int64_t x = x0 - V + int64_t(lane) * V;  // first element of this lane's vector
+    const int64_t za = zbeg + int64_t(bz) * zchunk;
+    const int64_t zb = za + zchunk < zend ? za + zchunk : zend;
+    const T* __restrict__ src = in + g.origin;
+    T* __restrict__ dst = out + g.origin;
+    const int64_t plane = g.plane;
+
+    // Zero the LDS pads once (they only ever feed discarded ring cells).
+    for (int i = threadIdx.y * 64 + threadIdx.x; i < 2 * LY * LX; i += 64 * NW) {
+        const int b = i / (LY * LX), rc = i % (LY * LX), rr = rc / LX, cc = rc % LX;
+        if (rr == 0 || rr == LY - 1 || cc < V || cc >= V + Tl::RW) {
+            lin[b][rr][cc] = T(0);
+            lt1[b][rr][cc] = T(0);
+        }
+    }
+
+    int64_t off[RY];
+    bool ldok[RY], yin[RY], st[RY];
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int rr = w + NW * k;  // region row
+        const int64_t y = y0 - 2 + rr;
+        off[k] = y * g.row + x;
+        ldok[k] = y >= -1 && y <= g.ny && x <= g.nx;
+        yin[k] = y >= 0 && y < g.ny;
+        st[k] = rr >= 2 && rr < RH - 2 && y < g.ny && lane >= 1 && lane <= 62;
+    }
+    bool xin[V], xst[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        xin[j] = x + j >= 0 && x + j < g.nx;
+        xst[j] = x + j < g.nx;
+    }
+    const int64_t zlast = zb + 1 < g.nz ? zb + 1 : g.nz;  // last input plane needed
+
+    VT vin[4][RY], vt1[4][RY];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < RY; ++k) {
+            vin[s][k] = VT{};
+            vt1[s][k] = VT{};
+        }
+
+    auto load_plane = [&](VT (&d)[RY], int64_t z) {
+        if (z >= -1 && z <= zlast) {
+#pragma unroll
+            for (int k = 0; k < RY; ++k)
+                if (ldok[k]) d[k] = *reinterpret_cast<const VT*>(src + z * plane + off[k]);
+        }
+    };
+
+    // slot of plane q = (q - za) & 3
+    load_plane(vin[2], za - 2);
+    load_plane(vin[3], za - 1);
+    load_plane(vin[0], za);
+    load_plane(vin[1], za + 1);
+    __syncthreads();  // LDS pads zeroed
+
+    auto step = [&](auto S_, int64_t p) {
+        constexpr int S = decltype(S_)::value;
+        constexpr int I0 = S, I1 = (S + 3) & 3, I2 = (S + 2) & 3;  // in(p), in(p-1), in(p-2)
+        constexpr int T1 = (S + 3) & 3, T2 = (S + 2) & 3, T3 = (S + 1) & 3;  // t1(p-1), t1(p-2), t1(p-3)
+        constexpr int B = S & 1, BP = B ^ 1;
+        const int xx = V + lane * V;
+        // 1. stage in(p-1)
+#pragma unroll
+        for (int k = 0; k < RY; ++k) *reinterpret_cast<VT*>(&lin[B][w + NW * k + 1][xx]) = vin[I1][k];
+        __syncthreads();
+        // 2. t1(p-1)
+        const int64_t z1 = p - 1;
+        const bool zin1 = z1 >= 0 && z1 < g.nz;
+#pragma unroll
+        for (int k = 0; k < RY; ++k) {
+            const int yy = w + NW * k + 1;
+            const T* cr = &lin[B][yy][xx];
+            const VT up = *reinterpret_cast<const VT*>(&lin[B][yy - 1][xx]);
+            const VT dn = *reinterpret_cast<const VT*>(&lin[B][yy + 1][xx]);
+            const T wl = cr[-1], er = cr[V];
+            const VT c = vin[I1][k], zm = vin[I2][k], zp = vin[I0][k];
+            VT o;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                T s = T(0);
+                s += j == 0 ? wl : c[j - 1];
+                s += j == V - 1 ? er : c[j + 1];
+                s += up[j];
+                s += dn[j];
+                s += zm[j];
+                s += zp[j];
+                o[j] = (zin1 && yin[k] && xin[j]) ? s * avg : c[j];
+            }
+            vt1[T1][k] = o;
+            *reinterpret_cast<VT*>(&lt1[B][yy][xx]) = o;
+        }
+        // 3. t2(p-2): neighbours of t1(p-2) were staged last iteration.
+        const int64_t z2 = p - 2;
+        if (z2 >= za) {
+#pragma unroll
+            for (int k = 0; k < RY; ++k) {
+                const int yy = w + NW * k + 1;
+                const T* cr = &lt1[BP][yy][xx];
+                const VT up = *reinterpret_cast<const VT*>(&lt1[BP][yy - 1][xx]);
+                const VT dn = *reinterpret_cast<const VT*>(&lt1[BP][yy + 1][xx]);
+                const T wl = cr[-1], er = cr[V];
+                const VT c = vt1[T2][k], zm = vt1[T3][k], zp = vt1[T1][k];
+                VT o;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    T s = T(0);
+                    s += j == 0 ? wl : c[j - 1];
+                    s += j == V - 1 ? er : c[j + 1];
+                    s += up[j];
+                    s += dn[j];
+                    s += zm[j];
+                    s += zp[j];
+                    o[j] = s * avg;
+                }
+                if (st[k]) {
+                    T* q = dst + z2 * plane + off[k];
+                    if (xst[V - 1]) {
+                        __builtin_nontemporal_store(o, reinterpret_cast<VT*>(q));
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < V; ++j)
+                            if (xst[j]) q[j] = o[j];
+                    }
+                }
+            }
+        }
+        // 4. prefetch in(p+2) into the slot of in(p-2), now dead
+        load_plane(vin[I2], p + 2);
+    };
+
+    for (int64_t p = za; p <= zb + 1; p += 4) {
+        step(std::integral_constant<int, 0>{}, p);
+        if (p + 1 <= zb + 1) step(std::integral_constant<int, 1>{}, p + 1);
+        if (p + 2 <= zb + 1) step(std::integral_constant<int, 2>{}, p + 2);
+        if (p + 3 <= zb + 1) step(std::integral_constant<int, 3>{}, p + 3);
+    }
+}
+
+int env_int(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    return s && *s ? std::atoi(s) : dflt;
+}
+
+template <typename T, int V, int RY, int NW>
+int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
+              hipStream_t s) {
+    using Tl = T2Tile<T, V, RY, NW>;
+    const Geom g = geom_of(l);
+    const int64_t nz = end - begin;
+    if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
+    const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
+    int zc = env_int("STENCIL_T2_ZCHUNK", 0);
+    if (zc <= 0) {
+        const int64_t tiles = gx * gy;
+        int64_t chunks = std::max<int64_t>(1, (env_int("STENCIL_T2_WG", 768) + tiles - 1) / tiles);
+        if (chunks >= 8) chunks = (chunks + 7) / 8 * 8;
+        chunks = std::min<int64_t>(chunks, nz);
+        zc = int((nz + chunks - 1) / chunks);
+        zc = std::max(zc, 8);
+    }
+    const int64_t gz = (nz + zc - 1) / zc;
+    const int64_t nb = gx * gy * gz;
+    if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for temporal2");
+    hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
+                       static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
+                       int(gy), int(gz), avg_weight<T>(l.prob));
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
+}  // namespace
+
+bool temporal2_supports(const stencil_problem& p) {
+    return p.dims == 3 && p.shape == STENCIL_STAR && p.radius == 1 &&
+           p.order == STENCIL_ORDER_NAIVE;
+}
+
+int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t begin,
+                     int64_t end, hipStream_t s) {
+    if (!temporal2_supports(l.prob))
+        return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 supports 3D star r=1 naive order only");
+    if (l.prob.dtype == STENCIL_F32) return launch_t2<float, 4, 4, 8>(l, in, out, begin, end, s);
+    return launch_t2<double, 2, 4, 8>(l, in, out, begin, end, s);
 }
 
 }  // namespace stencil

@@ -79,8 +79,9 @@ def test_2d_radius_random(gpu, r, order):
 
 # ------------------------------------------------------- 3D hot kernels
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("kernel", ["direct", "zmarch"])
-@pytest.mark.parametrize("shape3", [(64, 16, 8), (130, 37, 29), (1, 1, 1), (65, 17, 3), (200, 3, 70)])
+@pytest.mark.parametrize("kernel", ["direct", "zmarch", "temporal2"])
+@pytest.mark.parametrize("shape3", [(64, 16, 8), (130, 37, 29), (1, 1, 1), (65, 17, 3), (200, 3, 70), (124, 28, 2),
+                                    (249, 57, 11)])
 def test_3d_7pt_random_ragged(gpu, dtype, kernel, shape3):
     nx, ny, nz = shape3
     p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
@@ -88,6 +89,38 @@ def test_3d_7pt_random_ragged(gpu, dtype, kernel, shape3):
         want = ob.run(p, it, "random", 1234 + it)
         _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", kernel, nx, ny, nz, it, "random", 1234 + it)
         assert same_bits(got, want), (it, shape3)
+
+
+@pytest.mark.parametrize("zchunk", ["8", "9", "16"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype):
+    """Fused two-step launches with forced z-chunk sizes (chunk seams,
+    remainder chunks), odd iteration counts (a trailing single sweep)."""
+    monkeypatch.setenv("STENCIL_T2_ZCHUNK", zchunk)
+    nx, ny, nz = 131, 61, 29
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    for it in (2, 3, 6):
+        want = ob.run(p, it, "random", 99 + it)
+        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", "temporal2", nx, ny, nz, it, "random", 99 + it)
+        assert same_bits(got, want), it
+
+
+def test_sweep2_subrange(gpu):
+    """stencil_sweep2 on a slab sub-range equals two plain sweeps there."""
+    nx, ny, nz = 70, 33, 24
+    e = engine(gpu, 3, "fp64", "star", 1, "naive", "auto", nx, ny, nz)
+    e.reset("random", 5)
+    import torch
+    ref = e.a.clone()
+    # plain: two sweeps of the whole grid, then take planes [6, 18)
+    e.sweep(e.a, e.b, 0, nz)
+    e.sweep(e.b, ref, 0, nz)
+    e.reset("random", 5)
+    out = e.b
+    e.sweep2(e.a, out, 6, 18)
+    torch.cuda.synchronize()
+    gi, ri = e.interior(out), e.interior(ref)
+    assert torch.equal(gi[6:18], ri[6:18])
 
 
 @pytest.mark.parametrize("shape,r", [("box", 1), ("star", 2), ("star", 3), ("box", 2)])
