@@ -87,14 +87,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     n = args.n
-    spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=1, order="naive", kernel=args.kernel)
-    eng = JacobiEngine(spec, n, n, n, device=local)
+    # Multi-GPU slabs keep 2-deep z halos so pairs of sweeps fuse across the
+    # exchange too (one 2-plane exchange per fused pair).
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=1, order="naive", kernel=args.kernel,
+                       halo=2 if world > 1 else 0)
+    flags = (_lib.HALO_LO if rank > 0 else 0) | (_lib.HALO_HI if rank < world - 1 else 0)
+    eng = JacobiEngine(spec, n, n, n, device=local, flags=flags)
     slab = SlabJacobi(eng, SlabInfo(rank, world, rank * n, n), TorchDistExchanger(rank, world),
                       overlap=not args.no_overlap)
     slab.init("reference")
-    launches_per_sweep_unit, kernel_id = eng.plan(2)
-    sweeps_per_launch = 2 // launches_per_sweep_unit  # 2 for TEMPORAL2, else 1
-    kname = {1: "direct", 2: "zmarch", 3: "temporal2"}[kernel_id]
+    if world == 1:
+        launches2, kernel_id = eng.plan(2)
+        sweeps_per_launch = 2 // launches2  # 2 for TEMPORAL2, else 1
+        kname = {1: "direct", 2: "zmarch", 3: "temporal2"}[kernel_id]
+    else:
+        sweeps_per_launch = slab.launches_per_round()
+        kname = "temporal2" if slab.fused else "zmarch"
 
     def barrier():
         if world > 1:
@@ -132,7 +140,8 @@ def main():
     gcell = total_updates / elapsed / 1e9
     bytes_per_update = 2 * 8
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
-    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (n - 2) / n
+    edge = slab.depth if slab.fused else max(1, slab.depth)
+    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (n - 2 * edge) / n
     alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
     launch_ms = kernel_ms_total / max(1, kernel_launches)
     achieved = alg_bytes_launch / (launch_ms * 1e-3) / 1e9

@@ -98,6 +98,11 @@ enum {
     STENCIL_KERNEL_TEMPORAL2 = 3  /* ZMARCH with 2 fused time steps per launch */
 };
 enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
+/* stencil_problem.flags: which z faces of this grid are halos filled by a
+ * neighbouring slab (multi-GPU) rather than Dirichlet ghosts.  Only the fused
+ * two-step kernel cares: it must advance halo planes to t+1, and must keep
+ * Dirichlet ghost planes fixed. */
+enum { STENCIL_HALO_LO = 1, STENCIL_HALO_HI = 2 };
 
 typedef struct stencil_problem {
     int32_t dims;   /* 2 or 3 */
@@ -106,18 +111,22 @@ typedef struct stencil_problem {
     int32_t radius; /* >= 1 (reference -r) */
     int32_t order;  /* STENCIL_ORDER_* */
     int32_t kernel; /* STENCIL_KERNEL_* */
+    int32_t halo;   /* 3D: ghost planes per z side, >= radius (0 = radius); 2 for fused slabs */
+    int32_t flags;  /* STENCIL_HALO_* */
     int64_t nx, ny, nz; /* interior extents (reference: width = height = -s); nz = 1 for 2D */
 } stencil_problem;
 
-/* Device layout: x fastest, ghost ring of width `radius` on every axis the
- * problem has, rows padded so interior x = 0 of every row is 128-byte aligned.
+/* Device layout: x fastest, ghost ring of width `radius` on x and y and of
+ * `zghost` planes on z (3D), rows padded so interior x = 0 of every row is
+ * 128-byte aligned.
  * Element (x, y, z) of the interior (ghosts at -r..-1 and n..n+r-1) is at
  *   base[origin + z*plane + y*row + x]    (z = 0 for 2D). */
 typedef struct stencil_layout {
     stencil_problem prob;
     int64_t row;    /* elements between consecutive rows (y) */
     int64_t plane;  /* elements between consecutive planes (z); rows*row */
-    int64_t planes; /* allocated planes (nz + 2r for 3D, 1 for 2D) */
+    int64_t planes; /* allocated planes (nz + 2*zghost for 3D, 1 for 2D) */
+    int64_t zghost; /* ghost/halo planes per z side (3D; 0 for 2D) */
     int64_t rows;   /* allocated rows per plane (ny + 2r) */
     int64_t origin; /* element offset of interior (0,0,0) */
     int64_t elems;  /* elements to allocate */
@@ -150,7 +159,8 @@ int stencil_upload(const stencil_layout* l, void* dev, const void* host, int64_t
 int stencil_download(const stencil_layout* l, const void* dev, void* host, int64_t host_row,
                      int64_t host_rows, void* stream);
 /* Copy `count` planes (slow-axis units, ghost rows/planes included, indices
- * relative to the interior: -r .. n+r-1) between two device grids. */
+ * relative to the interior: -g .. n+g-1 with g = zghost in 3D, radius in 2D)
+ * between two device grids. */
 int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_first,
                         void* dst, int64_t dst_first, int64_t count, void* stream);
 

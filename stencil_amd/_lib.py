@@ -19,6 +19,7 @@ STAR, BOX = 0, 1
 ORDER_NAIVE, ORDER_DMA = 0, 1
 KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2 = 0, 1, 2, 3
 INIT_REFERENCE, INIT_RANDOM = 0, 1
+HALO_LO, HALO_HI = 1, 2
 
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2}
 
@@ -36,12 +37,14 @@ EXPORTED_SYMBOLS = (
 
 class Problem(Structure):
     _fields_ = [("dims", c_int32), ("dtype", c_int32), ("shape", c_int32), ("radius", c_int32),
-                ("order", c_int32), ("kernel", c_int32), ("nx", c_int64), ("ny", c_int64), ("nz", c_int64)]
+                ("order", c_int32), ("kernel", c_int32), ("halo", c_int32), ("flags", c_int32),
+                ("nx", c_int64), ("ny", c_int64), ("nz", c_int64)]
 
 
 class Layout(Structure):
     _fields_ = [("prob", Problem), ("row", c_int64), ("plane", c_int64), ("planes", c_int64),
-                ("rows", c_int64), ("origin", c_int64), ("elems", c_int64), ("bytes", c_int64)]
+                ("zghost", c_int64), ("rows", c_int64), ("origin", c_int64), ("elems", c_int64),
+                ("bytes", c_int64)]
 
 
 class MatrixView(Structure):
@@ -120,8 +123,8 @@ def check(rc: int, where: str) -> None:
 
 
 def make_problem(dims=3, dtype=F64, shape=STAR, radius=1, order=ORDER_NAIVE, kernel=KERNEL_AUTO,
-                 nx=1, ny=1, nz=1) -> Problem:
-    return Problem(dims, dtype, shape, radius, order, kernel, nx, ny, nz if dims == 3 else 1)
+                 nx=1, ny=1, nz=1, halo=0, flags=0) -> Problem:
+    return Problem(dims, dtype, shape, radius, order, kernel, halo, flags, nx, ny, nz if dims == 3 else 1)
 
 
 def make_layout(prob: Problem) -> Layout:

@@ -50,6 +50,10 @@ int check_problem(const stencil_problem* p) {
     if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_TEMPORAL2) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
     if (p->nx < 0 || p->ny < 0 || p->nz < 0) return set_error(STENCIL_EINVAL, "negative extent");
     if (p->dims == 2 && p->nz != 1) return set_error(STENCIL_EINVAL, "2D problems need nz = 1");
+    if (p->halo < 0 || (p->halo > 0 && p->halo < p->radius) || p->halo > 64)
+        return set_error(STENCIL_EINVAL, "halo must be 0 or in [radius, 64] (got %d)", p->halo);
+    if (p->dims == 2 && p->halo > p->radius) return set_error(STENCIL_EINVAL, "2D grids have radius-deep ghosts only");
+    if (p->flags & ~(STENCIL_HALO_LO | STENCIL_HALO_HI)) return set_error(STENCIL_EINVAL, "bad flags %d", p->flags);
     if (p->kernel == STENCIL_KERNEL_ZMARCH && !zmarch_supports(*p))
         return set_error(STENCIL_EUNSUPPORTED, "ZMARCH kernel supports 3D star r=1 naive order only");
     if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !temporal2_supports(*p))
@@ -94,7 +98,7 @@ __device__ __forceinline__ void u01(uint64_t u, double& d) { d = double(u >> 11)
 // ring) get 0; ghost cells follow stencil.cpp:190-207 generalised to 3D.
 template <typename T>
 __global__ void fill_initial_kernel(T* __restrict__ buf, Geom g, int64_t elems, int64_t row,
-                                    int64_t rows, int64_t origin_x, int r, int dims, int kind,
+                                    int64_t rows, int64_t origin_x, int r, int zg, int dims, int kind,
                                     uint64_t seed) {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= elems) return;
@@ -102,7 +106,7 @@ __global__ void fill_initial_kernel(T* __restrict__ buf, Geom g, int64_t elems, 
     const int64_t rem = i - pz * row * rows;
     const int64_t py = rem / row;
     const int64_t px = rem - py * row;
-    const int64_t x = px - origin_x, y = py - r, z = dims == 3 ? pz - r : 0;
+    const int64_t x = px - origin_x, y = py - r, z = dims == 3 ? pz - zg : 0;
     T v = T(0);
     const bool in_x = x >= -r && x < g.nx + r;
     if (in_x) {
@@ -154,12 +158,6 @@ __global__ void __launch_bounds__(256) copy_kernel(f32x4* __restrict__ dst, cons
         if (base + k * 256 < n) __builtin_nontemporal_store(v[k], dst + base + k * 256);
 }
 
-// Host pointer of the first allocated element of plane `p` (slow-axis
-// index, relative to the interior) and of its ghost corner.
-inline int64_t ghost_corner(const stencil_layout& l) {
-    const int r = l.prob.radius;
-    return l.origin - int64_t(r) * l.row - r - (l.prob.dims == 3 ? int64_t(r) * l.plane : 0);
-}
 
 }  // namespace
 }  // namespace stencil
@@ -195,8 +193,9 @@ int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     l.row = (origin_x + p.nx + r + align - 1) / align * align;
     l.rows = p.ny + 2 * r;
     l.plane = l.row * l.rows;
-    l.planes = p.dims == 3 ? p.nz + 2 * r : 1;
-    l.origin = (p.dims == 3 ? r * l.plane : 0) + r * l.row + origin_x;
+    l.zghost = p.dims == 3 ? std::max<int64_t>(r, p.halo) : 0;
+    l.planes = p.dims == 3 ? p.nz + 2 * l.zghost : 1;
+    l.origin = l.zghost * l.plane + r * l.row + origin_x;
     l.elems = l.plane * l.planes;
     l.bytes = l.elems * int64_t(elem_size(p));
     *out = l;
@@ -248,16 +247,16 @@ int stencil_fill_initial(const stencil_layout* l, void* dev, int init_kind, uint
         return set_error(STENCIL_EINVAL, "bad init kind %d", init_kind);
     const Geom g = geom_of(*l);
     const int64_t r = l->prob.radius;
-    const int64_t origin_x = l->origin - r * l->row - (l->prob.dims == 3 ? r * l->plane : 0);
+    const int64_t origin_x = l->origin - r * l->row - l->zghost * l->plane;
     const int64_t blocks = (l->elems + 255) / 256;
     if (l->prob.dtype == STENCIL_F32)
         hipLaunchKernelGGL(fill_initial_kernel<float>, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream),
                            static_cast<float*>(dev), g, l->elems, l->row, l->rows, origin_x, int(r),
-                           l->prob.dims, init_kind, seed);
+                           int(l->zghost), l->prob.dims, init_kind, seed);
     else
         hipLaunchKernelGGL(fill_initial_kernel<double>, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream),
                            static_cast<double*>(dev), g, l->elems, l->row, l->rows, origin_x, int(r),
-                           l->prob.dims, init_kind, seed);
+                           int(l->zghost), l->prob.dims, init_kind, seed);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
@@ -270,15 +269,18 @@ static int copy_grid(const stencil_layout* l, void* dev, const void* host_src, v
     const size_t es = elem_size(p);
     const int64_t width = p.nx + 2 * r, height = p.ny + 2 * r;
     if (host_row < width || host_rows < height) return set_error(STENCIL_EINVAL, "host array too small");
-    const int64_t corner = ghost_corner(*l);
-    for (int64_t z = 0; z < l->planes; ++z) {
-        char* d = static_cast<char*>(dev) + size_t(corner + z * l->plane) * es;
+    // Host planes cover z = -r .. nz+r-1 (3D) or the single 2D plane; device
+    // planes beyond the host's ghosts (zghost > r) are left untouched.
+    const int64_t hplanes = p.dims == 3 ? p.nz + 2 * r : 1;
+    for (int64_t hz = 0; hz < hplanes; ++hz) {
+        const int64_t z = p.dims == 3 ? hz - r : 0;
+        char* d = static_cast<char*>(dev) + size_t(l->origin + z * l->plane - r * l->row - r) * es;
         if (host_src) {
-            const char* h = static_cast<const char*>(host_src) + size_t(z * host_row * host_rows) * es;
+            const char* h = static_cast<const char*>(host_src) + size_t(hz * host_row * host_rows) * es;
             STENCIL_HIP_CHECK(hipMemcpy2DAsync(d, size_t(l->row) * es, h, size_t(host_row) * es, size_t(width) * es,
                                                size_t(height), hipMemcpyHostToDevice, as_stream(stream)));
         } else {
-            char* h = static_cast<char*>(host_dst) + size_t(z * host_row * host_rows) * es;
+            char* h = static_cast<char*>(host_dst) + size_t(hz * host_row * host_rows) * es;
             STENCIL_HIP_CHECK(hipMemcpy2DAsync(h, size_t(host_row) * es, d, size_t(l->row) * es, size_t(width) * es,
                                                size_t(height), hipMemcpyDeviceToHost, as_stream(stream)));
         }
@@ -299,7 +301,7 @@ int stencil_download(const stencil_layout* l, const void* dev, void* host, int64
 int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_first, void* dst, int64_t dst_first,
                         int64_t count, void* stream) {
     if (int rc = check_layout(l)) return rc;
-    const int64_t r = l->prob.radius;
+    const int64_t r = l->prob.dims == 3 ? l->zghost : l->prob.radius;
     const int64_t n = stencil_slow_extent(l);
     if (count < 0 || src_first < -r || dst_first < -r || src_first + count > n + r || dst_first + count > n + r)
         return set_error(STENCIL_EINVAL, "plane range out of bounds");
@@ -307,7 +309,7 @@ int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_fi
     const int64_t unit = l->prob.dims == 3 ? l->plane : l->row;
     // First allocated element of slow-axis index k: for 3D the whole plane,
     // for 2D the whole padded row.
-    const int64_t base = l->prob.dims == 3 ? r * l->plane : (l->origin - (l->origin % l->row));
+    const int64_t base = l->prob.dims == 3 ? l->zghost * l->plane : (l->origin - (l->origin % l->row));
     const char* s = static_cast<const char*>(src) + size_t(base + src_first * unit) * es;
     char* d = static_cast<char*>(dst) + size_t(base + dst_first * unit) * es;
     if (count == 0) return STENCIL_OK;

@@ -51,7 +51,8 @@ struct T2Tile {
 template <typename T, int V, int RY, int NW>
 __global__ void __launch_bounds__(64 * NW)
     temporal2_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
-                  int zchunk, int tiles_x, int tiles_y, int tiles_z, T avg) {
+                  int zchunk, int tiles_x, int tiles_y, int tiles_z, int64_t t1_lo, int64_t t1_hi,
+                  int64_t ld_lo, int64_t ld_hi, T avg) {
     using Tl = T2Tile<T, V, RY, NW>;
     using VT = typename Vec<T, V>::type;
     constexpr int TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
@@ -101,7 +102,10 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
-    const int64_t zlast = zb + 1 < g.nz ? zb + 1 : g.nz;  // last input plane needed
+    // t1 is computed on planes [t1_lo, t1_hi) (interior, plus halo planes of
+    // faces shared with a neighbouring slab) and copied elsewhere (Dirichlet
+    // ghost planes); input planes [ld_lo, min(zb + 1, ld_hi)] are loaded.
+    const int64_t zlast = zb + 1 < ld_hi ? zb + 1 : ld_hi;
 
     VT vin[4][RY], vt1[4][RY];
 #pragma unroll
@@ -113,7 +117,7 @@ __global__ void __launch_bounds__(64 * NW)
         }
 
     auto load_plane = [&](VT (&d)[RY], int64_t z) {
-        if (z >= -1 && z <= zlast) {
+        if (z >= ld_lo && z <= zlast) {
 #pragma unroll
             for (int k = 0; k < RY; ++k)
                 if (ldok[k]) d[k] = *reinterpret_cast<const VT*>(src + z * plane + off[k]);
@@ -139,7 +143,7 @@ __global__ void __launch_bounds__(64 * NW)
         __syncthreads();
         // 2. t1(p-1)
         const int64_t z1 = p - 1;
-        const bool zin1 = z1 >= 0 && z1 < g.nz;
+        const bool zin1 = z1 >= t1_lo && z1 < t1_hi;
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             const int yy = w + NW * k + 1;
@@ -235,9 +239,14 @@ int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int64_t gz = (nz + zc - 1) / zc;
     const int64_t nb = gx * gy * gz;
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for temporal2");
+    const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
+    if ((lo || hi) && l.zghost < 2)
+        return set_error(STENCIL_EINVAL, "fused steps across a slab halo need halo >= 2 (got %lld)", (long long)l.zghost);
+    const int64_t t1_lo = lo ? -1 : 0, t1_hi = hi ? g.nz + 1 : g.nz;
+    const int64_t ld_lo = lo ? -2 : -1, ld_hi = hi ? g.nz + 1 : g.nz;
     hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), avg_weight<T>(l.prob));
+                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }

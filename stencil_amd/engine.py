@@ -30,13 +30,21 @@ class StencilSpec:
     radius: int = 1
     order: str = "naive"         # "naive" | "dma"
     kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2"
+    halo: int = 0                # 3D ghost planes per z side (0 = radius); 2 for fused slabs
 
-    def problem(self, nx: int, ny: int, nz: int) -> _lib.Problem:
+    def problem(self, nx: int, ny: int, nz: int, flags: int = 0) -> _lib.Problem:
         return _lib.make_problem(
             dims=self.dims, dtype=_lib.F64 if self.dtype == "fp64" else _lib.F32,
             shape=_lib.BOX if self.shape == "box" else _lib.STAR, radius=self.radius,
             order=_lib.ORDER_DMA if self.order == "dma" else _lib.ORDER_NAIVE,
-            kernel=_lib.KERNEL_NAMES[self.kernel], nx=nx, ny=ny, nz=nz if self.dims == 3 else 1)
+            kernel=_lib.KERNEL_NAMES[self.kernel], nx=nx, ny=ny, nz=nz if self.dims == 3 else 1,
+            halo=self.halo, flags=flags)
+
+    @property
+    def fusable(self) -> bool:
+        """Does the fused two-step kernel cover this stencil?"""
+        return (self.dims == 3 and self.shape == "star" and self.radius == 1 and self.order == "naive"
+                and self.kernel in ("auto", "temporal2"))
 
     @property
     def elem_bytes(self) -> int:
@@ -53,14 +61,17 @@ class JacobiEngine:
     """Two grids (a, b) of one problem on one GPU."""
 
     def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int = 1, device: int | torch.device = 0,
-                 allocate: bool = True):
+                 allocate: bool = True, flags: int = 0):
         self.lib = _lib.load()
         self.spec = spec
-        self.prob = spec.problem(nx, ny, nz)
+        self.prob = spec.problem(nx, ny, nz, flags)
         self.layout = _lib.make_layout(self.prob)
         self.device = torch.device("cuda", device) if isinstance(device, int) else device
         self.torch_dtype = _TORCH_DTYPE[self.prob.dtype]
         self.r = spec.radius
+        # ghost/halo units per side of the slow axis (what a slab exchanges)
+        self.depth = int(self.layout.zghost) if spec.dims == 3 else spec.radius
+        self.fused = spec.fusable
         self.slow_extent = int(self.lib.stencil_slow_extent(ctypes.byref(self.layout)))
         # one slow-axis unit = a whole plane (3D) or a whole padded row (2D)
         self.unit = int(self.layout.plane if spec.dims == 3 else self.layout.row)
@@ -112,9 +123,8 @@ class JacobiEngine:
     def plane_view(self, grid: torch.Tensor, first: int, count: int) -> torch.Tensor:
         """Contiguous 1-D view of slow-axis units [first, first+count), ghost
         units included (first may be -r .. n+r-count)."""
-        r = self.r
         if self.spec.dims == 3:
-            base = r * int(self.layout.plane)
+            base = int(self.layout.zghost) * int(self.layout.plane)
         else:
             base = int(self.layout.origin) - int(self.layout.origin) % int(self.layout.row)
         start = base + first * self.unit

@@ -10,11 +10,15 @@ ghost planes per side, and one iteration exchanges r whole, contiguous planes
 with rank-1 and rank+1 -- no packing, and on an 8-GPU MI355X node every
 neighbour pair has its own xGMI link.
 
-Per iteration, on each rank (overlap=True):
-  stream A: sweep the 2r boundary planes -> post send/recv of them to the
+Per round, on each rank (overlap=True):
+  stream A: update the boundary planes -> post send/recv of them to the
             neighbours (torch.distributed P2P; RCCL on GPUs, gloo on CPUs);
-  stream B: sweep the interior planes meanwhile;
-  join:     the next sweep waits for both streams and the received halos.
+  stream B: update the interior planes meanwhile;
+  join:     the next round waits for both streams and the received halos.
+A round is one sweep (halo depth r), or -- when the backend has the fused
+two-step kernel and 2-deep halos -- two sweeps in one launch per plane range
+(temporal blocking across GPUs: the exchange of 2 planes every 2 sweeps, the
+halo plane itself advanced to t+1 on chip by the fused kernel).
 Every cell's arithmetic is the single-GPU kernel's, so results are bitwise
 identical for any number of ranks (tests/test_slab_gloo.py, tests/test_gpu_*).
 
@@ -76,9 +80,11 @@ class SlabJacobi:
         self.ex = exchanger
         self.overlap = overlap
         self.r = backend.r
+        self.depth = backend.depth  # planes exchanged per side
+        self.fused = bool(getattr(backend, "fused", False)) and self.depth >= 2
         n = slab.count
-        if slab.world > 1 and n < self.r:
-            raise ValueError(f"rank {slab.rank} owns {n} planes < radius {self.r}; use fewer ranks")
+        if slab.world > 1 and n < self.depth:
+            raise ValueError(f"rank {slab.rank} owns {n} planes < halo depth {self.depth}; use fewer ranks")
         self.cur, self.nxt = backend.a, backend.b
         self.on_gpu = self.cur.device.type == "cuda"
         self._timing = None  # list of (start, end) events around interior sweeps
@@ -88,9 +94,9 @@ class SlabJacobi:
 
     # -------------------------------------------------------------- helpers
     def _halo_views(self, grid):
-        n, r, be = self.slab.count, self.r, self.be
-        return (be.plane_view(grid, 0, r), be.plane_view(grid, n - r, r),
-                be.plane_view(grid, -r, r), be.plane_view(grid, n, r))
+        n, d, be = self.slab.count, self.depth, self.be
+        return (be.plane_view(grid, 0, d), be.plane_view(grid, n - d, d),
+                be.plane_view(grid, -d, d), be.plane_view(grid, n, d))
 
     def init(self, kind: str = "reference", seed: int = 0, plane_elems: int = 0) -> None:
         """Initial condition of the global grid restricted to this slab.
@@ -113,20 +119,22 @@ class SlabJacobi:
             torch.cuda.current_stream().synchronize()
 
     # ----------------------------------------------------------------- step
-    def step(self) -> None:
+    def _round(self, update, edge: int) -> None:
+        """One exchange round: `update(src, dst, b, e, stream)` advances planes
+        [b, e); `edge` = boundary planes updated first on each side."""
         src, dst = self.cur, self.nxt
-        n, r = self.slab.count, self.r
+        n = self.slab.count
         if self.slab.world == 1:
-            self.be.sweep(src, dst, 0, n)
-        elif not self.overlap or n <= 2 * r:
-            self.be.sweep(src, dst, 0, n)
+            update(src, dst, 0, n, None)
+        elif not self.overlap or n <= 2 * edge:
+            update(src, dst, 0, n, None)
             for w in self.ex.exchange(*self._halo_views(dst)):
                 w.wait()
         elif not self.on_gpu:
-            self.be.sweep(src, dst, 0, r)
-            self.be.sweep(src, dst, n - r, n)
+            update(src, dst, 0, edge, None)
+            update(src, dst, n - edge, n, None)
             works = self.ex.exchange(*self._halo_views(dst))
-            self.be.sweep(src, dst, r, n - r)
+            update(src, dst, edge, n - edge, None)
             for w in works:
                 w.wait()
         else:
@@ -135,15 +143,15 @@ class SlabJacobi:
             sa.wait_stream(main)
             sb.wait_stream(main)
             with torch.cuda.stream(sa):
-                self.be.sweep(src, dst, 0, r, stream=sa)
-                self.be.sweep(src, dst, n - r, n, stream=sa)
+                update(src, dst, 0, edge, sa)
+                update(src, dst, n - edge, n, sa)
                 works = self.ex.exchange(*self._halo_views(dst))
             with torch.cuda.stream(sb):
                 if self._timing is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev0.record(sb)
-                self.be.sweep(src, dst, r, n - r, stream=sb)
+                update(src, dst, edge, n - edge, sb)
                 if self._timing is not None:
                     ev1.record(sb)
                     self._timing.append((ev0, ev1))
@@ -152,6 +160,14 @@ class SlabJacobi:
             main.wait_stream(sa)
             main.wait_stream(sb)
         self.cur, self.nxt = dst, src
+
+    def step(self) -> None:
+        """One sweep."""
+        self._round(lambda s, d, b, e, st: self.be.sweep(s, d, b, e, stream=st), max(self.r, self.depth))
+
+    def step2(self) -> None:
+        """Two sweeps, fused (needs backend.fused and halo depth >= 2)."""
+        self._round(lambda s, d, b, e, st: self.be.sweep2(s, d, b, e, stream=st), self.depth)
 
     # ------------------------------------------------------- kernel timing
     def start_kernel_timing(self) -> None:
@@ -168,5 +184,14 @@ class SlabJacobi:
         return sum(a.elapsed_time(b) for a, b in ev), len(ev)
 
     def run(self, iterations: int) -> None:
-        for _ in range(iterations):
-            self.step()
+        if self.fused:
+            for _ in range(iterations // 2):
+                self.step2()
+            if iterations % 2:
+                self.step()
+        else:
+            for _ in range(iterations):
+                self.step()
+
+    def launches_per_round(self) -> int:
+        return 2 if self.fused else 1

@@ -43,7 +43,7 @@ def test_reference_struct_layouts():
     assert ctypes.sizeof(_lib.MatrixView) == 40
     assert ctypes.sizeof(_lib.Arguments) == 88
     assert _lib.Arguments.input.offset == 8 and _lib.Arguments.output.offset == 48
-    assert ctypes.sizeof(_lib.Problem) == 48
+    assert ctypes.sizeof(_lib.Problem) == 56
 
 
 @pytest.mark.parametrize("dims,dtype,r,n", [(2, _lib.F32, 1, (1024, 1024, 1)), (3, _lib.F64, 1, (512, 512, 512)),
@@ -72,17 +72,28 @@ def test_layout_alignment(dims, dtype, r, n):
     (dict(dims=2, nz=5), -1),
     (dict(dims=2, nz=1, kernel=_lib.KERNEL_ZMARCH), -5),
     (dict(dims=3, shape=_lib.BOX, kernel=_lib.KERNEL_ZMARCH), -5),
+    (dict(dims=3, radius=2, halo=1), -1),
+    (dict(dims=2, nz=1, halo=2), -1),
+    (dict(dims=3, flags=4), -1),
 ])
 def test_layout_rejects_invalid(kw, code):
     base = dict(dims=3, dtype=_lib.F64, nx=8, ny=8, nz=8)
     base.update(kw)
-    prob = _lib.Problem(base.get("dims"), base.get("dtype"), base.get("shape", 0), base.get("radius", 1),
-                        base.get("order", 0), base.get("kernel", 0), base.get("nx"), base.get("ny"), base.get("nz"))
+    prob = _lib.Problem(dims=base.get("dims"), dtype=base.get("dtype"), shape=base.get("shape", 0),
+                        radius=base.get("radius", 1), order=base.get("order", 0), kernel=base.get("kernel", 0),
+                        halo=base.get("halo", 0), flags=base.get("flags", 0),
+                        nx=base.get("nx"), ny=base.get("ny"), nz=base.get("nz"))
     lib = _lib.load()
     lay = _lib.Layout()
     rc = lib.stencil_layout_init(ctypes.byref(prob), ctypes.byref(lay))
     assert rc == code
     assert lib.stencil_last_error_message()
+
+
+def test_halo_depth_layout():
+    lay = _lib.make_layout(_lib.make_problem(dims=3, nx=16, ny=8, nz=10, halo=2, flags=_lib.HALO_LO))
+    assert lay.zghost == 2 and lay.planes == 14
+    assert lay.origin // lay.plane == 2
 
 
 def test_error_strings():
@@ -98,4 +109,10 @@ def test_plan_counts_launches():
     lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # AUTO fuses pairs
+    lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8, kernel=_lib.KERNEL_ZMARCH))
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_ZMARCH
+    lay = _lib.make_layout(_lib.make_problem(dims=3, shape=_lib.BOX, nx=8, ny=8, nz=8))
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 7 and kernel.value == _lib.KERNEL_DIRECT

@@ -1,0 +1,76 @@
+"""Slab decomposition with the HIP kernels, N logical slabs on one GPU.
+
+RCCL cannot put two ranks on one device, so the exchange here is a plain
+device copy between the slabs' grids (the torch.distributed exchange logic
+itself is covered by tests/test_slab_gloo.py).  What this pins is the GPU
+side of multi-GPU: 2-deep halos, the HALO_LO/HI flags of the fused kernel,
+boundary/interior plane ranges -- bitwise equal to one undivided grid."""
+import numpy as np
+import pytest
+import torch
+
+from stencil_amd import _lib
+from stencil_amd.engine import JacobiEngine, StencilSpec
+from stencil_amd.slab import partition
+
+pytestmark = pytest.mark.gpu
+
+
+def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split):
+    spec = StencilSpec(dims=3, dtype="fp64", halo=2)
+    engines, firsts = [], []
+    for r in range(world):
+        first, count = partition(nz, world, r)
+        flags = (_lib.HALO_LO if r > 0 else 0) | (_lib.HALO_HI if r < world - 1 else 0)
+        e = JacobiEngine(spec, nx, ny, count, device=gpu, flags=flags)
+        e.reset("random", 17 + first * nx * ny)
+        engines.append(e)
+        firsts.append((first, count))
+    cur = [e.a for e in engines]
+    nxt = [e.b for e in engines]
+
+    def exchange(grids):
+        for r in range(world - 1):
+            lo, hi = engines[r], engines[r + 1]
+            n_lo = firsts[r][1]
+            hi.plane_view(grids[r + 1], -2, 2).copy_(lo.plane_view(grids[r], n_lo - 2, 2))
+            lo.plane_view(grids[r], n_lo, 2).copy_(hi.plane_view(grids[r + 1], 0, 2))
+
+    exchange(cur)
+    done = 0
+    while done < iterations:
+        two = fused and iterations - done >= 2
+        for r, e in enumerate(engines):
+            n = firsts[r][1]
+            fn = e.sweep2 if two else e.sweep
+            if split and n > 4:
+                fn(cur[r], nxt[r], 0, 2)
+                fn(cur[r], nxt[r], n - 2, n)
+                fn(cur[r], nxt[r], 2, n - 2)
+            else:
+                fn(cur[r], nxt[r], 0, n)
+        exchange(nxt)
+        cur, nxt = nxt, cur
+        done += 2 if two else 1
+    torch.cuda.synchronize()
+    return torch.cat([e.interior(g) for e, g in zip(engines, cur)], dim=0)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("split", [False, True])
+def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split):
+    nx, ny, nz, it = 70, 45, 29, 7
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64"), nx, ny, nz, device=gpu)
+    ref.reset("random", 17)
+    fin, _ = ref.iterate(it)
+    want = ref.interior(fin)
+    got = run_slabs(gpu, nx, ny, nz, world, it, fused, split)
+    assert torch.equal(got, want)
+
+
+def test_fused_needs_deep_halo(gpu):
+    e = JacobiEngine(StencilSpec(dims=3, dtype="fp64"), 16, 16, 8, device=gpu, flags=_lib.HALO_LO)
+    e.reset()
+    with pytest.raises(_lib.StencilError):
+        e.sweep2(e.a, e.b, 0, 8)
