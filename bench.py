@@ -8,7 +8,8 @@ One step = one Jacobi sweep of the whole grid.  At N=1 the workload is
 BASELINE config 2 (512^3 interior, fp64, 7-point star; the default K=1000 is
 exactly its 1000 iterations).  At N>1 every rank owns a 512^3 Z-slab of a
 512 x 512 x 512N grid (weak scaling) and exchanges one halo plane with each
-neighbour per sweep over RCCL, overlapped with the interior sweep.
+neighbour per sweep over RCCL, overlapped with the interior sweep -- or, with
+the fused two-step kernel, two planes per pair of sweeps.
 
 Rank 0 prints one JSON line with the whole-job rate, the live roofline of the
 dominant kernel (algorithmic bytes per launch / average launch time from HIP
@@ -38,6 +39,10 @@ def parse():
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host"],
+                    help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal: every rank uses GPU 0 (needs --exchange host)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -75,16 +80,23 @@ def main():
 
     from stencil_amd import _lib
     from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
-    from stencil_amd.slab import SlabInfo, SlabJacobi, TorchDistExchanger
+    from stencil_amd.slab import HostStagedExchanger, SlabInfo, SlabJacobi, TorchDistExchanger
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.share_device:
+        if args.exchange != "host":
+            raise SystemExit("--share-device needs --exchange host (RCCL refuses two ranks on one GPU)")
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.exchange == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     n = args.n
     # Multi-GPU slabs keep 2-deep z halos so pairs of sweeps fuse across the
@@ -93,8 +105,8 @@ def main():
                        halo=2 if world > 1 else 0)
     flags = (_lib.HALO_LO if rank > 0 else 0) | (_lib.HALO_HI if rank < world - 1 else 0)
     eng = JacobiEngine(spec, n, n, n, device=local, flags=flags)
-    slab = SlabJacobi(eng, SlabInfo(rank, world, rank * n, n), TorchDistExchanger(rank, world),
-                      overlap=not args.no_overlap)
+    exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
+    slab = SlabJacobi(eng, SlabInfo(rank, world, rank * n, n), exchanger, overlap=not args.no_overlap)
     slab.init("reference")
     if world == 1:
         launches2, kernel_id = eng.plan(2)
@@ -130,7 +142,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.exchange == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
@@ -166,7 +178,9 @@ def main():
                             f"(global {n}x{n}x{n * world}), one step = one sweep",
                 "grid": [n, n, n * world],
                 "kernel": kname,
-                "parallelism": f"z-slab x{world}" + ("" if world == 1 else ", RCCL halo P2P overlapped"),
+                "parallelism": f"z-slab x{world}" + ("" if world == 1 else
+                                                     ", RCCL halo P2P overlapped" if args.exchange == "nccl"
+                                                     else ", host-staged gloo halo (rehearsal)"),
                 "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
             },
             "roofline": {

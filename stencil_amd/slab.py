@@ -63,6 +63,26 @@ class TorchDistExchanger:
         return dist.batch_isend_irecv(ops)
 
 
+class HostStagedExchanger(TorchDistExchanger):
+    """The same exchange through host memory over a CPU backend (gloo): lets
+    N ranks share one GPU, which RCCL refuses.  Used only to rehearse the
+    multi-rank path on a single-GPU box (bench.py --exchange host); blocking,
+    so it does not overlap."""
+
+    def exchange(self, send_lo, send_hi, recv_lo, recv_hi):
+        if send_lo.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        host = [t.cpu() for t in (send_lo, send_hi)]
+        rl, rh = torch.empty_like(host[0]), torch.empty_like(host[1])
+        for w in super().exchange(host[0], host[1], rl, rh):
+            w.wait()
+        if self.rank > 0:
+            recv_lo.copy_(rl)
+        if self.rank < self.world - 1:
+            recv_hi.copy_(rh)
+        return []
+
+
 @dataclass
 class SlabInfo:
     rank: int
