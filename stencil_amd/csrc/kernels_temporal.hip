@@ -76,12 +76,27 @@ __global__ void __launch_bounds__(64 * NW)
     T* __restrict__ dst = out + g.origin;
     const int64_t plane = g.plane;
 
-    // Zero the LDS pads once (they only ever feed discarded ring cells).
-    for (int i = threadIdx.y * 64 + threadIdx.x; i < 2 * LY * LX; i += 64 * NW) {
-        const int b = i / (LY * LX), rc = i % (LY * LX), rr = rc / LX, cc = rc % LX;
-        if (rr == 0 || rr == LY - 1 || cc < V || cc >= V + Tl::RW) {
-            lin[b][rr][cc] = T(0);
-            lt1[b][rr][cc] = T(0);
+    // Zero the LDS pads once (they only ever feed discarded ring cells):
+    // rows 0 and LY-1 whole, and V cells at both ends of every other row.
+    {
+        const int tid = threadIdx.y * 64 + threadIdx.x;
+        constexpr int NPAD = 2 * LX + (LY - 2) * 2 * V;
+        for (int i = tid; i < NPAD; i += 64 * NW) {
+            int rr, cc;
+            if (i < 2 * LX) {
+                rr = i < LX ? 0 : LY - 1;
+                cc = i % LX;
+            } else {
+                const int j = i - 2 * LX;
+                rr = 1 + j / (2 * V);
+                const int c = j % (2 * V);
+                cc = c < V ? c : Tl::RW + c;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                lin[b][rr][cc] = T(0);
+                lt1[b][rr][cc] = T(0);
+            }
         }
     }
 
@@ -262,8 +277,21 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
                      int64_t end, hipStream_t s) {
     if (!temporal2_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 supports 3D star r=1 naive order only");
-    if (l.prob.dtype == STENCIL_F32) return launch_t2<float, 4, 4, 8>(l, in, out, begin, end, s);
-    return launch_t2<double, 2, 4, 8>(l, in, out, begin, end, s);
+    // Workgroup shape RY rows per wave x NW waves (region 64V x RY*NW).
+    const int cfg = env_int("STENCIL_T2_CFG", 216);
+    if (l.prob.dtype == STENCIL_F32) {
+        switch (cfg) {
+        case 48: return launch_t2<float, 4, 4, 8>(l, in, out, begin, end, s);
+        case 28: return launch_t2<float, 4, 2, 8>(l, in, out, begin, end, s);
+        default: return launch_t2<float, 4, 2, 16>(l, in, out, begin, end, s);
+        }
+    }
+    switch (cfg) {
+    case 48: return launch_t2<double, 2, 4, 8>(l, in, out, begin, end, s);
+    case 28: return launch_t2<double, 2, 2, 8>(l, in, out, begin, end, s);
+    case 84: return launch_t2<double, 2, 8, 4>(l, in, out, begin, end, s);
+    default: return launch_t2<double, 2, 2, 16>(l, in, out, begin, end, s);
+    }
 }
 
 }  // namespace stencil
