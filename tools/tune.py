@@ -17,7 +17,9 @@ def main():
     kernel = os.environ.get("TUNE_KERNEL", "auto")
     dtype = os.environ.get("TUNE_DTYPE", "fp64")
     iters = int(os.environ.get("TUNE_ITERS", "50"))
-    eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel), n, n, n)
+    shape = [int(v) for v in os.environ.get("TUNE_SHAPE", f"{n},{n},{n}").split(",")]
+    eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel), *shape)
+    cells = shape[0] * shape[1] * shape[2]
     eng.reset()
     es = 8 if dtype == "fp64" else 4
     print(f"copy kernel: {copy_bandwidth(1 << 30, 20):.0f} GB/s", flush=True)
@@ -34,9 +36,9 @@ def main():
             res[i].append(ms / iters)
     for i, v in enumerate(variants):
         t = sorted(res[i])
-        gbs = n ** 3 * 2 * es / (t[0] * 1e-3) / 1e9
+        gbs = cells * 2 * es / (t[0] * 1e-3) / 1e9
         print(f"{json.dumps(v):60s} ms/sweep min {t[0]:.4f} med {t[len(t)//2]:.4f}  {gbs:.0f} GB/s alg  "
-              f"{n**3/(t[0]*1e-3)/1e9:.1f} Gcell/s", flush=True)
+              f"{cells/(t[0]*1e-3)/1e9:.1f} Gcell/s", flush=True)
 
 
 if __name__ == "__main__":
