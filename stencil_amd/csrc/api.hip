@@ -54,10 +54,10 @@ int check_problem(const stencil_problem* p) {
         return set_error(STENCIL_EINVAL, "halo must be 0 or in [radius, 64] (got %d)", p->halo);
     if (p->dims == 2 && p->halo > p->radius) return set_error(STENCIL_EINVAL, "2D grids have radius-deep ghosts only");
     if (p->flags & ~(STENCIL_HALO_LO | STENCIL_HALO_HI)) return set_error(STENCIL_EINVAL, "bad flags %d", p->flags);
-    if (p->kernel == STENCIL_KERNEL_ZMARCH && !zmarch_supports(*p))
-        return set_error(STENCIL_EUNSUPPORTED, "ZMARCH kernel supports 3D star r=1 naive order only");
-    if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !temporal2_supports(*p))
-        return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 kernel does not support this problem");
+    if (p->kernel == STENCIL_KERNEL_ZMARCH && !march_supported(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "ZMARCH kernels cover 3D r=1 naive star (7-pt) and box (27-pt) only");
+    if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !fused_supported(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 kernels cover 3D r=1 naive star (7-pt) and box (27-pt) only");
     return STENCIL_OK;
 }
 
@@ -69,17 +69,27 @@ int check_layout(const stencil_layout* l) {
 // Resolve AUTO to a concrete single-sweep kernel family.
 int sweep_family(const stencil_problem& p) {
     if (p.kernel == STENCIL_KERNEL_DIRECT) return STENCIL_KERNEL_DIRECT;
-    if (zmarch_supports(p)) return STENCIL_KERNEL_ZMARCH;
+    if (march_supported(p)) return STENCIL_KERNEL_ZMARCH;
     return STENCIL_KERNEL_DIRECT;
 }
 
 // Does stencil_iterate fuse pairs of sweeps?  Explicit TEMPORAL2, or AUTO on
-// a problem the fused kernel supports (STENCIL_NO_T2=1 disables the latter).
+// a problem a fused kernel supports (STENCIL_NO_T2=1 disables the latter).
 bool iterate_fused(const stencil_problem& p) {
     if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
-    if (p.kernel != STENCIL_KERNEL_AUTO || !temporal2_supports(p)) return false;
+    if (p.kernel != STENCIL_KERNEL_AUTO || !fused_supported(p)) return false;
     const char* e = std::getenv("STENCIL_NO_T2");
     return !(e && *e && *e != '0');
+}
+
+int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
+    if (sweep_family(l.prob) == STENCIL_KERNEL_ZMARCH)
+        return zmarch_supports(l.prob) ? launch_zmarch(l, in, out, b, e, s) : launch_box27(l, in, out, b, e, 1, s);
+    return launch_direct(l, in, out, b, e, s);
+}
+
+int launch_fused(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
+    return temporal2_supports(l.prob) ? launch_temporal2(l, in, out, b, e, s) : launch_box27(l, in, out, b, e, 2, s);
 }
 
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
@@ -322,22 +332,18 @@ int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t be
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range [%lld, %lld) out of bounds", (long long)begin, (long long)end);
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported (Jacobi ping-pong)");
-    int rc;
-    if (sweep_family(l->prob) == STENCIL_KERNEL_ZMARCH)
-        rc = launch_zmarch(*l, in, out, begin, end, as_stream(stream));
-    else
-        rc = launch_direct(*l, in, out, begin, end, as_stream(stream));
+    const int rc = launch_single(*l, in, out, begin, end, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();
     return rc;
 }
 
 int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end, void* stream) {
     if (int rc = check_layout(l)) return rc;
-    if (!temporal2_supports(l->prob)) return set_error(STENCIL_EUNSUPPORTED, "no fused two-step kernel for this problem");
+    if (!fused_supported(l->prob)) return set_error(STENCIL_EUNSUPPORTED, "no fused two-step kernel for this problem");
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
-    int rc = launch_temporal2(*l, in, out, begin, end, as_stream(stream));
+    const int rc = launch_fused(*l, in, out, begin, end, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();
     return rc;
 }
@@ -373,14 +379,13 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         // holding the result no longer follows the one-sweep parity rule; the
         // caller learns where it is through *final_in_b.
         for (; i + 2 <= iterations && rc == STENCIL_OK; i += 2) {
-            rc = launch_temporal2(*l, in, out, 0, n, s);
+            rc = launch_fused(*l, in, out, 0, n, s);
             std::swap(in, out);
             swapped = !swapped;
         }
     }
     for (; i < iterations && rc == STENCIL_OK; ++i) {
-        rc = sweep_family(l->prob) == STENCIL_KERNEL_ZMARCH ? launch_zmarch(*l, in, out, 0, n, s)
-                                                             : launch_direct(*l, in, out, 0, n, s);
+        rc = launch_single(*l, in, out, 0, n, s);
         std::swap(in, out);
         swapped = !swapped;
     }

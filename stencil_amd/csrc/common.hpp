@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "stencil_hip.h"
@@ -67,5 +68,13 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
                      int64_t end, hipStream_t s);
 bool zmarch_supports(const stencil_problem& p);
 bool temporal2_supports(const stencil_problem& p);
+int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
+                 int steps, hipStream_t s);
+bool box27_supports(const stencil_problem& p);
+
+// Kernel-family coverage: the z-marching single-sweep family (7-point star
+// and 27-point box, r = 1) and the fused two-step family (same stencils).
+inline bool march_supported(const stencil_problem& p) { return zmarch_supports(p) || box27_supports(p); }
+inline bool fused_supported(const stencil_problem& p) { return temporal2_supports(p) || box27_supports(p); }
 
 }  // namespace stencil

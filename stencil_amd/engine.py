@@ -43,7 +43,7 @@ class StencilSpec:
     @property
     def fusable(self) -> bool:
         """Does the fused two-step kernel cover this stencil?"""
-        return (self.dims == 3 and self.shape == "star" and self.radius == 1 and self.order == "naive"
+        return (self.dims == 3 and self.radius == 1 and self.order == "naive"
                 and self.kernel in ("auto", "temporal2"))
 
     @property

@@ -71,7 +71,8 @@ def test_layout_alignment(dims, dtype, r, n):
     (dict(nx=-3), -1),
     (dict(dims=2, nz=5), -1),
     (dict(dims=2, nz=1, kernel=_lib.KERNEL_ZMARCH), -5),
-    (dict(dims=3, shape=_lib.BOX, kernel=_lib.KERNEL_ZMARCH), -5),
+    (dict(dims=3, shape=_lib.BOX, radius=2, kernel=_lib.KERNEL_ZMARCH), -5),
+    (dict(dims=3, radius=2, kernel=_lib.KERNEL_TEMPORAL2), -5),
     (dict(dims=3, radius=2, halo=1), -1),
     (dict(dims=2, nz=1, halo=2), -1),
     (dict(dims=3, flags=4), -1),
@@ -114,5 +115,8 @@ def test_plan_counts_launches():
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_ZMARCH
     lay = _lib.make_layout(_lib.make_problem(dims=3, shape=_lib.BOX, nx=8, ny=8, nz=8))
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # 27-point fuses too
+    lay = _lib.make_layout(_lib.make_problem(dims=3, radius=2, nx=8, ny=8, nz=8))
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_DIRECT

@@ -78,31 +78,45 @@ def test_2d_radius_random(gpu, r, order):
 
 
 # ------------------------------------------------------- 3D hot kernels
+@pytest.mark.parametrize("stencil", ["star", "box"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("kernel", ["direct", "zmarch", "temporal2"])
 @pytest.mark.parametrize("shape3", [(64, 16, 8), (130, 37, 29), (1, 1, 1), (65, 17, 3), (200, 3, 70), (124, 28, 2),
                                     (249, 57, 11)])
-def test_3d_7pt_random_ragged(gpu, dtype, kernel, shape3):
+def test_3d_r1_random_ragged(gpu, stencil, dtype, kernel, shape3):
+    """7-point star and 27-point box, r = 1, every kernel family."""
     nx, ny, nz = shape3
-    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    p = ob.problem(3, dtype, stencil, 1, "naive", nx, ny, nz)
     for it in (1, 2, 5):
         want = ob.run(p, it, "random", 1234 + it)
-        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", kernel, nx, ny, nz, it, "random", 1234 + it)
+        _, got = gpu_run(gpu, 3, dtype, stencil, 1, "naive", kernel, nx, ny, nz, it, "random", 1234 + it)
         assert same_bits(got, want), (it, shape3)
 
 
 @pytest.mark.parametrize("zchunk", ["8", "9", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype):
+@pytest.mark.parametrize("stencil", ["star", "box"])
+def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype, stencil):
     """Fused two-step launches with forced z-chunk sizes (chunk seams,
     remainder chunks), odd iteration counts (a trailing single sweep)."""
     monkeypatch.setenv("STENCIL_T2_ZCHUNK", zchunk)
+    monkeypatch.setenv("STENCIL_BOX_ZCHUNK", zchunk)
     nx, ny, nz = 131, 61, 29
-    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    p = ob.problem(3, dtype, stencil, 1, "naive", nx, ny, nz)
     for it in (2, 3, 6):
         want = ob.run(p, it, "random", 99 + it)
-        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", "temporal2", nx, ny, nz, it, "random", 99 + it)
+        _, got = gpu_run(gpu, 3, dtype, stencil, 1, "naive", "temporal2", nx, ny, nz, it, "random", 99 + it)
         assert same_bits(got, want), it
+
+
+@pytest.mark.parametrize("cfg", ["0", "212"])
+def test_box_fused_shapes(gpu, monkeypatch, cfg):
+    monkeypatch.setenv("STENCIL_BOX_CFG", cfg)
+    nx, ny, nz = 150, 47, 21
+    p = ob.problem(3, "fp64", "box", 1, "naive", nx, ny, nz)
+    want = ob.run(p, 4, "random", 3)
+    _, got = gpu_run(gpu, 3, "fp64", "box", 1, "naive", "temporal2", nx, ny, nz, 4, "random", 3)
+    assert same_bits(got, want)
 
 
 def test_sweep2_subrange(gpu):

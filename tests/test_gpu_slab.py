@@ -16,8 +16,8 @@ from stencil_amd.slab import partition
 pytestmark = pytest.mark.gpu
 
 
-def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split):
-    spec = StencilSpec(dims=3, dtype="fp64", halo=2)
+def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star"):
+    spec = StencilSpec(dims=3, dtype="fp64", halo=2, shape=shape)
     engines, firsts = [], []
     for r in range(world):
         first, count = partition(nz, world, r)
@@ -56,16 +56,17 @@ def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split):
     return torch.cat([e.interior(g) for e, g in zip(engines, cur)], dim=0)
 
 
+@pytest.mark.parametrize("shape", ["star", "box"])
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("split", [False, True])
-def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split):
+def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split, shape):
     nx, ny, nz, it = 70, 45, 29, 7
-    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64"), nx, ny, nz, device=gpu)
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", shape=shape, kernel="direct"), nx, ny, nz, device=gpu)
     ref.reset("random", 17)
     fin, _ = ref.iterate(it)
     want = ref.interior(fin)
-    got = run_slabs(gpu, nx, ny, nz, world, it, fused, split)
+    got = run_slabs(gpu, nx, ny, nz, world, it, fused, split, shape)
     assert torch.equal(got, want)
 
 
