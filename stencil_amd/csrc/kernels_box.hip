@@ -50,8 +50,12 @@ __global__ void __launch_bounds__(64 * NW)
     using Tl = BoxTile<T, V, RY, NW, STEPS>;
     using VT = typename BVec<T, V>::type;
     constexpr int TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY, RW = Tl::RW;
-    constexpr int NL = STEPS == 2 ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) T lds[NL][2][LY][LX];
+    // Input planes rotate through 4 LDS buffers (slot = plane mod 4): a plane
+    // is read at its own iteration and at the next one, so its buffer must
+    // not be rewritten before two barriers have passed.  t1 planes (STEPS=2)
+    // are read only one iteration after being written: 2 buffers.
+    __shared__ __attribute__((aligned(16))) T lin[4][LY][LX];
+    __shared__ __attribute__((aligned(16))) T lt1[STEPS == 2 ? 2 : 1][LY][LX];
 
     const int nb = tiles_x * tiles_y * tiles_z;
     int t = blockIdx.x;
@@ -84,9 +88,11 @@ __global__ void __launch_bounds__(64 * NW)
                 cc = c < V ? c : RW + c;
             }
 #pragma unroll
-            for (int l = 0; l < NL; ++l)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) lds[l][b][rr][cc] = T(0);
+            for (int b = 0; b < 4; ++b) lin[b][rr][cc] = T(0);
+            if constexpr (STEPS == 2) {
+                lt1[0][rr][cc] = T(0);
+                lt1[1][rr][cc] = T(0);
+            }
         }
     }
 
@@ -183,7 +189,7 @@ __global__ void __launch_bounds__(64 * NW)
         }
     };
 
-    // Iteration q: LDS_in[B] <- in(q) (LDS_in[B^1] still holds in(q-1)).
+    // Iteration q: LDS_in[q] <- in(q) (LDS_in[q-1] still holds in(q-1)).
     //  stage 1: finish plane q-1 (+9 terms of plane q) and build plane q from
     //           scratch (9 terms of plane q-1, then 8 of plane q): one running
     //           sum per cell is carried to the next iteration.
@@ -195,7 +201,7 @@ __global__ void __launch_bounds__(64 * NW)
         constexpr int B = S & 1, BP = B ^ 1;
         const int xx = V + lane * V;
 #pragma unroll
-        for (int k = 0; k < RY; ++k) *reinterpret_cast<VT*>(&lds[0][B][w + NW * k + 1][xx]) = vin[CQ][k];
+        for (int k = 0; k < RY; ++k) *reinterpret_cast<VT*>(&lin[CQ][w + NW * k + 1][xx]) = vin[CQ][k];
         load_plane(vin[CP], q + 3);  // slot of q-1: in(q-1) now lives in LDS_in[BP]
         __syncthreads();
         const bool st_fin = q - 1 >= s1_lo && q - 1 < s1_hi;
@@ -207,12 +213,12 @@ __global__ void __launch_bounds__(64 * NW)
             VT nw;
             if (st_new) {  // 9 terms of plane q-1 first (one neighbourhood live at a time)
                 T np[3][V + 2];
-                hood(lds[0][BP], yy, np);
+                hood(lin[CP], yy, np);
 #pragma unroll
                 for (int j = 0; j < V; ++j) nw[j] = add9(T(0), np, j);
             }
             T nq[3][V + 2];
-            hood(lds[0][B], yy, nq);
+            hood(lin[CQ], yy, nq);
             if (st_fin) {
                 VT fin, o;
 #pragma unroll
@@ -222,10 +228,10 @@ __global__ void __launch_bounds__(64 * NW)
                     for (int j = 0; j < V; ++j) o[j] = fin[j] * avg;
                     if (st[k]) store_out(o, q - 1, k);
                 } else {
-                    const VT c = *reinterpret_cast<const VT*>(&lds[0][BP][yy][xx]);  // in(q-1)
+                    const VT c = *reinterpret_cast<const VT*>(&lin[CP][yy][xx]);  // in(q-1)
 #pragma unroll
                     for (int j = 0; j < V; ++j) o[j] = (zin1 && yin[k] && xin[j]) ? fin[j] * avg : c[j];
-                    *reinterpret_cast<VT*>(&lds[NL - 1][B][yy][xx]) = o;
+                    *reinterpret_cast<VT*>(&lt1[B][yy][xx]) = o;
                 }
             }
             if (st_new) {
@@ -244,7 +250,7 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
                 for (int k = 0; k < RY; ++k) {
                     T nv[3][V + 2];
-                    hood(lds[NL - 1][BP], w + NW * k + 1, nv);
+                    hood(lt1[BP], w + NW * k + 1, nv);
                     VT o;
 #pragma unroll
                     for (int j = 0; j < V; ++j) {
@@ -322,7 +328,6 @@ int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t beg
     }
     if (steps == 2) {
         switch (cfg) {
-        case 212: return launch_box<double, 2, 2, 12, 2>(l, in, out, begin, end, s);
         default: return launch_box<double, 2, 1, 16, 2>(l, in, out, begin, end, s);
         }
     }
