@@ -18,7 +18,8 @@ def main():
     dtype = os.environ.get("TUNE_DTYPE", "fp64")
     iters = int(os.environ.get("TUNE_ITERS", "50"))
     shape = [int(v) for v in os.environ.get("TUNE_SHAPE", f"{n},{n},{n}").split(",")]
-    eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel), *shape)
+    stencil = os.environ.get("TUNE_STENCIL", "star")
+    eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel, shape=stencil), *shape)
     cells = shape[0] * shape[1] * shape[2]
     eng.reset()
     es = 8 if dtype == "fp64" else 4
