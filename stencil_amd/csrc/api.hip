@@ -77,7 +77,9 @@ int sweep_family(const stencil_problem& p) {
 // a problem a fused kernel supports (STENCIL_NO_T2=1 disables the latter).
 bool iterate_fused(const stencil_problem& p) {
     if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
-    if (p.kernel != STENCIL_KERNEL_AUTO || !fused_supported(p)) return false;
+    // AUTO fuses the 7-point star only: the fused 27-point kernel is slower
+    // than its single sweep on MI355X.
+    if (p.kernel != STENCIL_KERNEL_AUTO || !temporal2_supports(p)) return false;
     const char* e = std::getenv("STENCIL_NO_T2");
     return !(e && *e && *e != '0');
 }

@@ -48,7 +48,7 @@ struct T2Tile {
     static constexpr int LY = RH + 2;      // LDS rows: pad | region RH | pad
 };
 
-template <typename T, int V, int RY, int NW>
+template <typename T, int V, int RY, int NW, int R = 4>
 __global__ void __launch_bounds__(64 * NW)
     temporal2_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
                   int zchunk, int tiles_x, int tiles_y, int tiles_z, int64_t t1_lo, int64_t t1_hi,
@@ -122,9 +122,13 @@ __global__ void __launch_bounds__(64 * NW)
     // ghost planes); input planes [ld_lo, min(zb + 1, ld_hi)] are loaded.
     const int64_t zlast = zb + 1 < ld_hi ? zb + 1 : ld_hi;
 
-    VT vin[4][RY], vt1[4][RY];
+    // Register rings of R slots (slot of plane q = (q - za) mod R): input
+    // planes p-2 .. p+R-3 (plane p+R-2 is loaded as soon as p-2 is dead, so a
+    // load has R-2 iterations to land) and t1 planes p-3 .. p-1.
+    static_assert(R % 2 == 0 && R >= 4, "ring size must be even (LDS parity) and >= 4");
+    VT vin[R][RY], vt1[R][RY];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < R; ++s)
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             vin[s][k] = VT{};
@@ -139,17 +143,14 @@ __global__ void __launch_bounds__(64 * NW)
         }
     };
 
-    // slot of plane q = (q - za) & 3
-    load_plane(vin[2], za - 2);
-    load_plane(vin[3], za - 1);
-    load_plane(vin[0], za);
-    load_plane(vin[1], za + 1);
+#pragma unroll
+    for (int i = -2; i <= R - 3; ++i) load_plane(vin[(i + R) % R], za + i);
     __syncthreads();  // LDS pads zeroed
 
     auto step = [&](auto S_, int64_t p) {
         constexpr int S = decltype(S_)::value;
-        constexpr int I0 = S, I1 = (S + 3) & 3, I2 = (S + 2) & 3;  // in(p), in(p-1), in(p-2)
-        constexpr int T1 = (S + 3) & 3, T2 = (S + 2) & 3, T3 = (S + 1) & 3;  // t1(p-1), t1(p-2), t1(p-3)
+        constexpr int I0 = S, I1 = (S + R - 1) % R, I2 = (S + R - 2) % R;  // in(p), in(p-1), in(p-2)
+        constexpr int T1 = I1, T2 = I2, T3 = (S + R - 3) % R;             // t1(p-1), t1(p-2), t1(p-3)
         constexpr int B = S & 1, BP = B ^ 1;
         const int xx = V + lane * V;
         // 1. stage in(p-1)
@@ -217,15 +218,19 @@ __global__ void __launch_bounds__(64 * NW)
                 }
             }
         }
-        // 4. prefetch in(p+2) into the slot of in(p-2), now dead
-        load_plane(vin[I2], p + 2);
+        // 4. load in(p+R-2) into the slot of in(p-2), now dead
+        load_plane(vin[I2], p + R - 2);
     };
 
-    for (int64_t p = za; p <= zb + 1; p += 4) {
+    for (int64_t p = za; p <= zb + 1; p += R) {
         step(std::integral_constant<int, 0>{}, p);
         if (p + 1 <= zb + 1) step(std::integral_constant<int, 1>{}, p + 1);
         if (p + 2 <= zb + 1) step(std::integral_constant<int, 2>{}, p + 2);
         if (p + 3 <= zb + 1) step(std::integral_constant<int, 3>{}, p + 3);
+        if constexpr (R > 4) {
+            if (p + 4 <= zb + 1) step(std::integral_constant<int, 4 % R>{}, p + 4);
+            if (p + 5 <= zb + 1) step(std::integral_constant<int, 5 % R>{}, p + 5);
+        }
     }
 }
 
@@ -234,7 +239,7 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW>
+template <typename T, int V, int RY, int NW, int R = 4>
 int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
               hipStream_t s) {
     using Tl = T2Tile<T, V, RY, NW>;
@@ -259,7 +264,7 @@ int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin,
         return set_error(STENCIL_EINVAL, "fused steps across a slab halo need halo >= 2 (got %lld)", (long long)l.zghost);
     const int64_t t1_lo = lo ? -1 : 0, t1_hi = hi ? g.nz + 1 : g.nz;
     const int64_t ld_lo = lo ? -2 : -1, ld_hi = hi ? g.nz + 1 : g.nz;
-    hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
+    hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW, R>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
                        int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();

@@ -43,8 +43,10 @@ class StencilSpec:
     @property
     def fusable(self) -> bool:
         """Does the fused two-step kernel cover this stencil?"""
-        return (self.dims == 3 and self.radius == 1 and self.order == "naive"
-                and self.kernel in ("auto", "temporal2"))
+        if self.dims != 3 or self.radius != 1 or self.order != "naive":
+            return False
+        # the fused 27-point kernel is slower than its single sweep (DESIGN.md §5): explicit only
+        return self.kernel == "temporal2" or (self.kernel == "auto" and self.shape == "star")
 
     @property
     def elem_bytes(self) -> int:
