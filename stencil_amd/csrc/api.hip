@@ -56,8 +56,9 @@ int check_problem(const stencil_problem* p) {
     if (p->flags & ~(STENCIL_HALO_LO | STENCIL_HALO_HI)) return set_error(STENCIL_EINVAL, "bad flags %d", p->flags);
     if (p->kernel == STENCIL_KERNEL_ZMARCH && !march_supported(*p))
         return set_error(STENCIL_EUNSUPPORTED, "ZMARCH kernels cover 3D r=1 naive star (7-pt) and box (27-pt) only");
-    if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !fused_supported(*p))
-        return set_error(STENCIL_EUNSUPPORTED, "TEMPORAL2 kernels cover 3D r=1 naive star (7-pt) and box (27-pt) only");
+    if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !fused_supported(*p) && !tb2d_supports(*p))
+        return set_error(STENCIL_EUNSUPPORTED,
+                         "TEMPORAL2 kernels cover 3D r=1 naive star/box and 2D star r<=4 only");
     return STENCIL_OK;
 }
 
@@ -82,6 +83,15 @@ bool iterate_fused(const stencil_problem& p) {
     if (p.kernel != STENCIL_KERNEL_AUTO || !temporal2_supports(p)) return false;
     const char* e = std::getenv("STENCIL_NO_T2");
     return !(e && *e && *e != '0');
+}
+
+// 2D problems iterate K sweeps per launch with the tile resident in LDS
+// (kernels_tb2d.hip) unless a single-sweep family is forced.
+bool iterate_tb2d(const stencil_problem& p) {
+    if (!tb2d_supports(p)) return false;
+    if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
+    const char* e = std::getenv("STENCIL_NO_T2");
+    return p.kernel == STENCIL_KERNEL_AUTO && !(e && *e && *e != '0');
 }
 
 int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
@@ -352,7 +362,13 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
 
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {
     if (int rc = check_layout(l)) return rc;
-    const bool t2 = iterate_fused(l->prob);
+    if (iterate_tb2d(l->prob)) {
+        const int64_t k = tb2d_max_steps(l->prob);
+        if (launches) *launches = (int64_t(iterations) + k - 1) / k;
+        if (kernel) *kernel = STENCIL_KERNEL_TEMPORAL2;
+        return STENCIL_OK;
+    }
+    const bool t2 = !iterate_tb2d(l->prob) && iterate_fused(l->prob);
     if (launches) *launches = t2 ? int64_t(iterations / 2 + iterations % 2) : int64_t(iterations);
     if (kernel) *kernel = t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
     return STENCIL_OK;
@@ -373,9 +389,17 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
     const bool t2 = iterate_fused(l->prob);
     void* in = a;
     void* out = b;
-    bool swapped = false;
     uint32_t i = 0;
     int rc = STENCIL_OK;
+    if (iterate_tb2d(l->prob)) {
+        const uint32_t k = uint32_t(tb2d_max_steps(l->prob));
+        for (; i < iterations && rc == STENCIL_OK;) {
+            const uint32_t n2 = std::min(k, iterations - i);
+            rc = launch_tb2d(*l, in, out, int(n2), s);
+            std::swap(in, out);
+            i += n2;
+        }
+    }
     if (t2) {
         // A fused pair reads `in` and writes S(S(in)) to `out`, so the buffer
         // holding the result no longer follows the one-sweep parity rule; the
@@ -383,13 +407,11 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         for (; i + 2 <= iterations && rc == STENCIL_OK; i += 2) {
             rc = launch_fused(*l, in, out, 0, n, s);
             std::swap(in, out);
-            swapped = !swapped;
         }
     }
     for (; i < iterations && rc == STENCIL_OK; ++i) {
         rc = launch_single(*l, in, out, 0, n, s);
         std::swap(in, out);
-        swapped = !swapped;
     }
     if (rc != STENCIL_OK) return rc;
     if (final_in_b) *final_in_b = in == b ? 1 : 0;
@@ -400,7 +422,6 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }
-    (void)swapped;
     clear_error();
     return STENCIL_OK;
 }

@@ -71,6 +71,9 @@ bool temporal2_supports(const stencil_problem& p);
 int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
                  int steps, hipStream_t s);
 bool box27_supports(const stencil_problem& p);
+int launch_tb2d(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s);
+bool tb2d_supports(const stencil_problem& p);
+int tb2d_max_steps(const stencil_problem& p);
 
 // Kernel-family coverage: the z-marching single-sweep family (7-point star
 // and 27-point box, r = 1) and the fused two-step family (same stencils).
