@@ -50,70 +50,77 @@ __device__ __forceinline__ T cell2d(const T* c, int row, T avg) {
     }
 }
 
-constexpr int kThreads = 512;
+constexpr int kWaves = 4;
+constexpr int kRX = 64;  // region width: one column per lane
+constexpr int kRY = 32;  // region height: kRY / kWaves rows per wave
 
-// Region RX x RY cells (RX a multiple of 64), LDS row stride RX + 1 (odd
-// stride spreads a column over banks).
-template <typename T, int ORDER, int R, int RX, int RY>
-__global__ void __launch_bounds__(kThreads)
+// LDS row stride kRX + 1 keeps a column's cells on different banks.
+template <typename T, int ORDER, int R>
+__global__ void __launch_bounds__(64 * kWaves)
     tb2d(const T* __restrict__ in, T* __restrict__ out, Geom g, int steps, int tiles_x, T avg) {
-    constexpr int LXS = RX + 1;
-    __shared__ T buf[2][RY][LXS];
-    const int K = steps;
-    const int ring = K * R;
-    const int TX = RX - 2 * ring, TY = RY - 2 * ring;
+    constexpr int LXS = kRX + 1;
+    constexpr int RPW = kRY / kWaves;  // rows per wave
+    __shared__ T buf[2][kRY][LXS];
+    const int ring = steps * R;
+    const int TX = kRX - 2 * ring, TY = kRY - 2 * ring;
     const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
-    const int64_t x0 = int64_t(bx) * TX - ring, y0 = int64_t(by) * TY - ring;  // region origin (interior coords)
+    const int64_t x0 = int64_t(bx) * TX - ring, y0 = int64_t(by) * TY - ring;  // region origin
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x = x0 + lane;
+    const bool xin = x >= 0 && x < g.nx;
+    const bool xld = x >= -R && x < g.nx + R;
     const T* __restrict__ src = in + g.origin;
     T* __restrict__ dst = out + g.origin;
 
-    // load the region into both buffers (ghost cells and out-of-grid cells
-    // are never written by the sweeps, so both buffers must hold them)
-    for (int i = threadIdx.x; i < RX * RY; i += kThreads) {
-        const int ry = i / RX, rx = i % RX;
-        const int64_t y = y0 + ry, x = x0 + rx;
+    // Both buffers get the whole region: ghost and out-of-grid cells are
+    // never written by a sweep.
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const int ry = w + kWaves * j;
+        const int64_t y = y0 + ry;
         T v = T(0);
-        if (x >= -R && x < g.nx + R && y >= -R && y < g.ny + R) v = src[y * g.row + x];
-        buf[0][ry][rx] = v;
-        buf[1][ry][rx] = v;
+        if (xld && y >= -R && y < g.ny + R) v = src[y * g.row + x];
+        buf[0][ry][lane] = v;
+        buf[1][ry][lane] = v;
     }
     __syncthreads();
 
     int cur = 0;
-    for (int s = 1; s <= K; ++s) {
-        const int lo = s * R;  // step s updates region cells [lo, R?-lo)
-        const int wx = RX - 2 * lo, wy = RY - 2 * lo;
+    for (int s = 1; s <= steps; ++s) {
+        const int lo = s * R;
+        const bool cx = xin && lane >= lo && lane < kRX - lo;
         const T* a = &buf[cur][0][0];
         T* b = &buf[cur ^ 1][0][0];
-        for (int i = threadIdx.x; i < wx * wy; i += kThreads) {
-            const int ry = lo + i / wx, rx = lo + i % wx;
-            const int64_t y = y0 + ry, x = x0 + rx;
-            if (x >= 0 && x < g.nx && y >= 0 && y < g.ny)
-                b[ry * LXS + rx] = cell2d<T, ORDER, R>(a + ry * LXS + rx, LXS, avg);
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int ry = w + kWaves * j;
+            const int64_t y = y0 + ry;
+            if (cx && ry >= lo && ry < kRY - lo && y >= 0 && y < g.ny)
+                b[ry * LXS + lane] = cell2d<T, ORDER, R>(a + ry * LXS + lane, LXS, avg);
         }
         cur ^= 1;
         __syncthreads();
     }
 
-    for (int i = threadIdx.x; i < TX * TY; i += kThreads) {
-        const int ty = i / TX, tx = i % TX;
-        const int64_t y = y0 + ring + ty, x = x0 + ring + tx;
-        if (x < g.nx && y < g.ny) dst[y * g.row + x] = buf[cur][ring + ty][ring + tx];
+    const bool sx = lane >= ring && lane < ring + TX && x < g.nx;
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const int ry = w + kWaves * j;
+        const int64_t y = y0 + ry;
+        if (sx && ry >= ring && ry < ring + TY && y < g.ny) dst[y * g.row + x] = buf[cur][ry][lane];
     }
 }
 
 template <typename T, int ORDER, int R>
 int launch_tb(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
-    // 64 KB of LDS per buffer: fp64 128 x 64 cells, fp32 256 x 64 cells.
-    constexpr int RX = sizeof(T) == 8 ? 128 : 256, RY = 63;
     const Geom g = geom_of(l);
     if (g.nx <= 0 || g.ny <= 0 || steps <= 0) return STENCIL_OK;
     const int ring = steps * R;
-    const int TX = RX - 2 * ring, TY = RY - 2 * ring;
-    if (TX < 8 || TY < 8) return set_error(STENCIL_EINVAL, "tb2d: %d steps of radius %d leave no tile", steps, R);
+    const int TX = kRX - 2 * ring, TY = kRY - 2 * ring;
+    if (TX < 4 || TY < 4) return set_error(STENCIL_EINVAL, "tb2d: %d steps of radius %d leave no tile", steps, R);
     const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
     if (tx * ty > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "tb2d: grid too large");
-    hipLaunchKernelGGL((tb2d<T, ORDER, R, RX, RY>), dim3(unsigned(tx * ty)), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((tb2d<T, ORDER, R>), dim3(unsigned(tx * ty)), dim3(64, kWaves), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, steps, int(tx), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
@@ -138,9 +145,9 @@ bool tb2d_supports(const stencil_problem& p) {
 
 int tb2d_max_steps(const stencil_problem& p) {
     const char* e = std::getenv("STENCIL_TB2D_K");
-    int k = e && *e ? std::atoi(e) : 8;
-    // keep the output tile at least ~half the 63-row region
-    const int cap = std::max(1, 16 / p.radius);
+    int k = e && *e ? std::atoi(e) : 4;
+    // keep the output tile at least half the 32-row region
+    const int cap = std::max(1, 8 / p.radius);
     return std::max(1, std::min(k, cap));
 }
 
