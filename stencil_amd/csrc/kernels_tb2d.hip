@@ -145,7 +145,7 @@ bool tb2d_supports(const stencil_problem& p) {
 
 int tb2d_max_steps(const stencil_problem& p) {
     const char* e = std::getenv("STENCIL_TB2D_K");
-    int k = e && *e ? std::atoi(e) : 4;
+    int k = e && *e ? std::atoi(e) : 8;
     // keep the output tile at least half the 32-row region
     const int cap = std::max(1, 8 / p.radius);
     return std::max(1, std::min(k, cap));

@@ -110,7 +110,7 @@ def test_plan_counts_launches():
     lay2 = _lib.make_layout(_lib.make_problem(dims=2, nx=64, ny=64))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay2), 100, ctypes.byref(launches), ctypes.byref(kernel)) == 0
-    assert launches.value == 25 and kernel.value == _lib.KERNEL_TEMPORAL2  # 2D: 4 sweeps per launch in LDS
+    assert launches.value == 13 and kernel.value == _lib.KERNEL_TEMPORAL2  # 2D: 8 sweeps per launch in LDS
     lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
