@@ -54,13 +54,17 @@ constexpr int kWaves = 4;
 constexpr int kRX = 64;  // region width: one column per lane
 constexpr int kRY = 32;  // region height: kRY / kWaves rows per wave
 
-// LDS row stride kRX + 1 keeps a column's cells on different banks.
+// LDS image of the region with an R-cell pad on every side, so every
+// neighbour read of every lane is in bounds: the sweep is computed for all
+// rows unconditionally (all LDS reads of a step can be in flight together)
+// and only the stores are predicated.
 template <typename T, int ORDER, int R>
 __global__ void __launch_bounds__(64 * kWaves)
     tb2d(const T* __restrict__ in, T* __restrict__ out, Geom g, int steps, int tiles_x, T avg) {
-    constexpr int LXS = kRX + 1;
+    constexpr int LXS = kRX + 2 * R + 1;  // odd stride: a column spreads over banks
+    constexpr int LYS = kRY + 2 * R;
     constexpr int RPW = kRY / kWaves;  // rows per wave
-    __shared__ T buf[2][kRY][LXS];
+    __shared__ T buf[2][LYS * LXS];
     const int ring = steps * R;
     const int TX = kRX - 2 * ring, TY = kRY - 2 * ring;
     const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
@@ -71,17 +75,31 @@ __global__ void __launch_bounds__(64 * kWaves)
     const bool xld = x >= -R && x < g.nx + R;
     const T* __restrict__ src = in + g.origin;
     T* __restrict__ dst = out + g.origin;
+    auto at = [&](int ry) { return (ry + R) * LXS + R + lane; };
 
-    // Both buffers get the whole region: ghost and out-of-grid cells are
-    // never written by a sweep.
+    // Zero the pads (read only by discarded lanes), then load the region into
+    // both buffers: ghost and out-of-grid cells are never written by a sweep.
+    for (int i = threadIdx.y * 64 + lane; i < LYS * LXS; i += 64 * kWaves) {
+        const int py = i / LXS, px = i % LXS;
+        if (py < R || py >= R + kRY || px < R || px >= R + kRX) {
+            buf[0][i] = T(0);
+            buf[1][i] = T(0);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
         const int ry = w + kWaves * j;
         const int64_t y = y0 + ry;
         T v = T(0);
         if (xld && y >= -R && y < g.ny + R) v = src[y * g.row + x];
-        buf[0][ry][lane] = v;
-        buf[1][ry][lane] = v;
+        buf[0][at(ry)] = v;
+        buf[1][at(ry)] = v;
+    }
+    bool yin[RPW];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const int64_t y = y0 + w + kWaves * j;
+        yin[j] = y >= 0 && y < g.ny;
     }
     __syncthreads();
 
@@ -89,14 +107,15 @@ __global__ void __launch_bounds__(64 * kWaves)
     for (int s = 1; s <= steps; ++s) {
         const int lo = s * R;
         const bool cx = xin && lane >= lo && lane < kRX - lo;
-        const T* a = &buf[cur][0][0];
-        T* b = &buf[cur ^ 1][0][0];
+        const T* a = buf[cur];
+        T* b = buf[cur ^ 1];
+        T v[RPW];
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) v[j] = cell2d<T, ORDER, R>(a + at(w + kWaves * j), LXS, avg);
 #pragma unroll
         for (int j = 0; j < RPW; ++j) {
             const int ry = w + kWaves * j;
-            const int64_t y = y0 + ry;
-            if (cx && ry >= lo && ry < kRY - lo && y >= 0 && y < g.ny)
-                b[ry * LXS + lane] = cell2d<T, ORDER, R>(a + ry * LXS + lane, LXS, avg);
+            if (cx && yin[j] && ry >= lo && ry < kRY - lo) b[at(ry)] = v[j];
         }
         cur ^= 1;
         __syncthreads();
@@ -107,7 +126,7 @@ __global__ void __launch_bounds__(64 * kWaves)
     for (int j = 0; j < RPW; ++j) {
         const int ry = w + kWaves * j;
         const int64_t y = y0 + ry;
-        if (sx && ry >= ring && ry < ring + TY && y < g.ny) dst[y * g.row + x] = buf[cur][ry][lane];
+        if (sx && ry >= ring && ry < ring + TY && y < g.ny) dst[y * g.row + x] = buf[cur][at(ry)];
     }
 }
 
