@@ -7,6 +7,7 @@
 #include <exception>
 #include <iostream>
 #include <ratio>
+#include <string>
 #include <string_view>
 
 #include "program_options.hpp"
@@ -44,6 +45,14 @@ void run_test(std::string_view method_name, ProgramOptions const& options) {
     for (unsigned i = 0; i != options.repeat_count; ++i) {
         Stencil stencil(options);
         auto const duration = stencil.run(method_name);
+        if (duration && !options.bmp.empty() && i + 1 == options.repeat_count) {
+            std::string path = options.bmp;
+            if (options.method_names.size() > 1) path += "." + std::string(method_name) + ".bmp";
+            if (!stencil.to_bmp(path)) {
+                std::cerr << "could not write " << path << "\n";
+                g_status = 4;
+            }
+        }
         if (!duration) {
             std::cerr << "Unknown method: " << method_name << "\n";
             g_status = 2;

@@ -123,6 +123,8 @@ auto ProgramOptions::parse(int argc, char** argv) -> std::optional<ProgramOption
          [&](const std::string& v) { if (v != "reference" && v != "random") return false; r.random_init = v == "random"; return true; }},
         {0, "print-config", Kind::Flag, false, "[ext] Print the parsed options and exit.",
          [&](const std::string&) { r.print_config = true; return true; }},
+        {0, "bmp", Kind::Str, false, "[ext] Write the final grid of each method as a BMP (FILE, or FILE.<method>.bmp for several methods).",
+         [&](const std::string& v) { r.bmp = v; return !v.empty(); }},
         {0, "seed", Kind::Int64, false, "[ext] Seed of --init random.",
          [&](const std::string& v) { int64_t s; if (!parse_i64(v, s)) return false; r.seed = uint64_t(s); return true; }},
     };

@@ -38,6 +38,7 @@ struct ProgramOptions {
     bool random_init = false;      // --init reference|random
     uint64_t seed = 0x5EED;        // --seed N
     bool print_config = false;     // --print-config: print the parsed options and exit 0
+    std::string bmp;               // --bmp FILE: dump the final grid of each method (f4)
 
     int64_t extent_x() const { return nx >= 0 ? nx : matrix_size; }
     int64_t extent_y() const { return ny >= 0 ? ny : matrix_size; }

@@ -7,6 +7,7 @@
 #include <string>
 #include <unordered_map>
 
+#include "bmp.hpp"
 #include "stencil_hip.h"
 
 namespace {
@@ -223,4 +224,21 @@ bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& 
 
 auto Stencil::check_result() const -> bool {
     return options.fp64 ? check_typed(matrix64, result64) : check_typed(matrix32, result32);
+}
+
+template <class T>
+bool Stencil::bmp_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result, const std::string& path) const {
+    // The final grid is where the parity rule put it (stencil.cpp:134).
+    const BoundaryGrid<T>& g = (options.iterations & 1u) ? result : matrix;
+    if (g.empty()) return false;
+    const int64_t z = g.depth() / 2;
+    std::vector<BmpPixel> px;
+    px.reserve(size_t(g.width() * g.height()));
+    for (int64_t y = 0; y < g.height(); ++y)
+        for (int64_t x = 0; x < g.width(); ++x) px.push_back(heat_color(double(g.elem_at(z, y, x))));
+    return write_bmp24(path, uint32_t(g.width()), uint32_t(g.height()), px);
+}
+
+auto Stencil::to_bmp(const std::string& path) const -> bool {
+    return options.fp64 ? bmp_typed(matrix64, result64, path) : bmp_typed(matrix32, result32, path);
 }

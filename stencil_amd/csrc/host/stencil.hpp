@@ -9,6 +9,7 @@
 
 #include <chrono>
 #include <optional>
+#include <string>
 #include <string_view>
 
 #include "grid.hpp"
@@ -41,6 +42,10 @@ public:
 
     auto check_result() const -> bool;
 
+    /// Write the final grid of the last run as a 24-bit BMP (2D: the grid;
+    /// 3D: the middle z plane), colour map of stencil.cpp:153-188.
+    auto to_bmp(const std::string& path) const -> bool;
+
     /// Device time of the last run (hipEvents around the launches), ms.
     double last_device_ms() const { return device_ms; }
     /// Interior cell count (one iteration updates each once).
@@ -59,4 +64,6 @@ private:
     bool check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const;
     template <class T>
     void init_typed(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) const;
+    template <class T>
+    bool bmp_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result, const std::string& path) const;
 };

@@ -241,3 +241,15 @@ def test_cli_check_result_on_gpu(gpu):
                          timeout=300)
     assert out.returncode == 0, out.stderr + out.stdout
     assert out.stdout.count("is correct.") == 3
+
+
+def test_cli_bmp_dump(gpu, tmp_path):
+    cli = os.path.join(ROOT, "build", "bin", "stencil_main")
+    out = tmp_path / "grid.bmp"
+    p = subprocess.run([cli, "-s", "50", "-b", "8", "-i", "200", "-m", "HIP", "--bmp", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    data = out.read_bytes()
+    assert data[:2] == b"BM" and len(data) == 54 + 50 * (150 + 2)
+    # x-ghost columns are 1 -> the cells next to them are warm (red channel set)
+    assert data[54 + 2] > 0
