@@ -251,5 +251,8 @@ def test_cli_bmp_dump(gpu, tmp_path):
     assert p.returncode == 0, p.stderr
     data = out.read_bytes()
     assert data[:2] == b"BM" and len(data) == 54 + 50 * (150 + 2)
-    # x-ghost columns are 1 -> the cells next to them are warm (red channel set)
-    assert data[54 + 2] > 0
+    # x-ghost columns are 1 -> the cell next to them is no longer cold (green > 0),
+    # the centre of the grid still is (pure blue)
+    assert data[54 + 1] > 0
+    mid = 54 + 25 * 152 + 25 * 3
+    assert data[mid:mid + 3] == bytes([255, 0, 0])
