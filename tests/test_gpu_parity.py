@@ -251,8 +251,21 @@ def test_cli_bmp_dump(gpu, tmp_path):
     assert p.returncode == 0, p.stderr
     data = out.read_bytes()
     assert data[:2] == b"BM" and len(data) == 54 + 50 * (150 + 2)
-    # x-ghost columns are 1 -> the cell next to them is no longer cold (green > 0),
-    # the centre of the grid still is (pure blue)
-    assert data[54 + 1] > 0
-    mid = 54 + 25 * 152 + 25 * 3
-    assert data[mid:mid + 3] == bytes([255, 0, 0])
+    # every pixel is the heat-map colour of the oracle's final grid
+    p = ob.problem(2, "fp32", "star", 1, "naive", 50, 50)
+    grid = ob.interior(p, ob.run(p, 200)).astype(np.float64)
+
+    def heat(v):
+        v = min(max(v, 0.0), 1.0)
+        if v < 0.25:
+            return (255, int(4 * v * 255), 0)
+        if v < 0.5:
+            return (int((1 + 4 * (0.25 - v)) * 255), 255, 0)
+        if v < 0.75:
+            return (0, 255, int(4 * (v - 0.5) * 255))
+        return (0, int((1 + 4 * (0.75 - v)) * 255), 255)
+
+    for y in range(50):
+        row = data[54 + y * 152: 54 + y * 152 + 150]
+        want = b"".join(bytes(heat(float(grid[y, x]))) for x in range(50))
+        assert row == want, y
