@@ -341,8 +341,16 @@ int stencil_copy_planes(const stencil_layout* l, const void* src, int64_t src_fi
 
 int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end, void* stream) {
     if (int rc = check_layout(l)) return rc;
-    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
-        return set_error(STENCIL_EINVAL, "sweep range [%lld, %lld) out of bounds", (long long)begin, (long long)end);
+    // A 3D slab may also advance the halo planes of a face shared with a
+    // neighbour (HALO_LO/HI) as deep as its ghost layers allow beyond the
+    // stencil radius: two sweeps per 2-plane exchange (communication-avoiding
+    // temporal blocking, stencil_amd/slab.py).
+    const int64_t ext = l->prob.dims == 3 ? l->zghost - l->prob.radius : 0;
+    const int64_t lo = (l->prob.flags & STENCIL_HALO_LO) ? -ext : 0;
+    const int64_t hi = stencil_slow_extent(l) + ((l->prob.flags & STENCIL_HALO_HI) ? ext : 0);
+    if (begin < lo || end > hi || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range [%lld, %lld) out of bounds [%lld, %lld)", (long long)begin,
+                         (long long)end, (long long)lo, (long long)hi);
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported (Jacobi ping-pong)");
     const int rc = launch_single(*l, in, out, begin, end, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();

@@ -301,7 +301,11 @@ int launch_box(const stencil_layout& l, const void* in, void* out, int64_t begin
     if (STEPS == 2 && (lo || hi) && l.zghost < 2)
         return set_error(STENCIL_EINVAL, "fused steps across a slab halo need halo >= 2");
     const int64_t t1_lo = (STEPS == 2 && lo) ? -1 : 0, t1_hi = (STEPS == 2 && hi) ? g.nz + 1 : g.nz;
-    const int64_t ld_lo = (STEPS == 2 && lo) ? -2 : -1, ld_hi = (STEPS == 2 && hi) ? g.nz + 1 : g.nz;
+    int64_t ld_lo = (STEPS == 2 && lo) ? -2 : -1, ld_hi = (STEPS == 2 && hi) ? g.nz + 1 : g.nz;
+    if (STEPS == 1) {  // single sweeps may cover slab-halo planes (stencil_sweep): load what they read
+        ld_lo = std::min<int64_t>(ld_lo, begin - 1);
+        ld_hi = std::max<int64_t>(ld_hi, end);
+    }
     hipLaunchKernelGGL((box27_zmarch<T, V, RY, NW, STEPS>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
                        int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));

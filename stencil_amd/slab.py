@@ -189,6 +189,56 @@ class SlabJacobi:
         """Two sweeps, fused (needs backend.fused and halo depth >= 2)."""
         self._round(lambda s, d, b, e, st: self.be.sweep2(s, d, b, e, stream=st), self.depth)
 
+    def step2_split(self) -> None:
+        """Two single sweeps per exchange of 2 planes (halo depth >= 2): the
+        first sweep also advances the 1-deep halo planes of shared faces, the
+        second the owned planes -- communication-avoiding temporal blocking
+        with the single-sweep kernel (used where no fused kernel is faster).
+        The result lands back in the current grid."""
+        src, dst = self.cur, self.nxt
+        n, be, sl = self.slab.count, self.be, self.slab
+        lo = -1 if sl.rank > 0 else 0
+        hi = n + 1 if sl.rank < sl.world - 1 else n
+        B = 2  # planes exchanged = second-sweep boundary thickness
+        if sl.world == 1:
+            be.sweep(src, dst, 0, n)
+            be.sweep(dst, src, 0, n)
+        elif not self.overlap or not self.on_gpu or n <= 2 * B + 2:
+            be.sweep(src, dst, lo, hi)
+            be.sweep(dst, src, 0, n)
+            for w in self.ex.exchange(*self._halo_views(src)):
+                w.wait()
+        else:
+            main = torch.cuda.current_stream()
+            sa, sb = self.stream_bnd, self.stream_int
+            sa.wait_stream(main)
+            sb.wait_stream(main)
+            first_done = torch.cuda.Event()
+            with torch.cuda.stream(sa):
+                be.sweep(src, dst, lo, B + 1, stream=sa)
+                be.sweep(src, dst, n - B - 1, hi, stream=sa)
+                first_done.record(sa)
+                be.sweep(dst, src, 0, B, stream=sa)
+                be.sweep(dst, src, n - B, n, stream=sa)
+                works = self.ex.exchange(*self._halo_views(src))
+            with torch.cuda.stream(sb):
+                if self._timing is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record(sb)
+                # reads src planes [B, n-B): disjoint from what stream A's
+                # second sweep writes ([0, B) and [n-B, n))
+                be.sweep(src, dst, B + 1, n - B - 1, stream=sb)
+                if self._timing is not None:  # time the interior launch alone
+                    ev1.record(sb)
+                    self._timing.append((ev0, ev1))
+                sb.wait_event(first_done)
+                be.sweep(dst, src, B, n - B, stream=sb)
+            for w in works:
+                w.wait()
+            main.wait_stream(sa)
+            main.wait_stream(sb)
+
     # ------------------------------------------------------- kernel timing
     def start_kernel_timing(self) -> None:
         """Record HIP events on the interior stream around every interior
@@ -203,10 +253,28 @@ class SlabJacobi:
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in ev), len(ev)
 
-    def run(self, iterations: int) -> None:
+    @property
+    def mode(self) -> str:
+        """'fused' (two sweeps per launch), 'split2' (two single sweeps per
+        2-plane exchange) or 'single' (one sweep per 1-plane exchange)."""
         if self.fused:
+            return "fused"
+        if self.depth >= 2 * self.r and self.r == 1 and self.split2:
+            return "split2"
+        return "single"
+
+    split2 = True  # allow the communication-avoiding 2-sweep rounds
+
+    def run(self, iterations: int) -> None:
+        mode = self.mode
+        if mode == "fused":
             for _ in range(iterations // 2):
                 self.step2()
+            if iterations % 2:
+                self.step()
+        elif mode == "split2":
+            for _ in range(iterations // 2):
+                self.step2_split()
             if iterations % 2:
                 self.step()
         else:
@@ -214,4 +282,5 @@ class SlabJacobi:
                 self.step()
 
     def launches_per_round(self) -> int:
+        """Sweeps per timed interior launch (the bench's roofline unit)."""
         return 2 if self.fused else 1

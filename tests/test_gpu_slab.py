@@ -16,7 +16,7 @@ from stencil_amd.slab import partition
 pytestmark = pytest.mark.gpu
 
 
-def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star"):
+def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star", split2=False):
     spec = StencilSpec(dims=3, dtype="fp64", halo=2, shape=shape)
     engines, firsts = [], []
     for r in range(world):
@@ -38,6 +38,16 @@ def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star"):
 
     exchange(cur)
     done = 0
+    if split2:  # two single sweeps per 2-plane exchange, halo planes advanced by the first
+        while done + 2 <= iterations:
+            for r, e in enumerate(engines):
+                n = firsts[r][1]
+                lo = -1 if r > 0 else 0
+                hi = n + 1 if r < world - 1 else n
+                e.sweep(cur[r], nxt[r], lo, hi)
+                e.sweep(nxt[r], cur[r], 0, n)
+            exchange(cur)
+            done += 2
     while done < iterations:
         two = fused and iterations - done >= 2
         for r, e in enumerate(engines):
@@ -68,6 +78,24 @@ def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split, shape):
     want = ref.interior(fin)
     got = run_slabs(gpu, nx, ny, nz, world, it, fused, split, shape)
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_split2_rounds_bitwise(gpu, world, shape):
+    nx, ny, nz, it = 70, 45, 29, 7
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", shape=shape, kernel="direct"), nx, ny, nz, device=gpu)
+    ref.reset("random", 17)
+    fin, _ = ref.iterate(it)
+    got = run_slabs(gpu, nx, ny, nz, world, it, False, False, shape, split2=True)
+    assert torch.equal(got, ref.interior(fin))
+
+
+def test_sweep_range_into_halo_needs_flag(gpu):
+    e = JacobiEngine(StencilSpec(dims=3, dtype="fp64", halo=2), 16, 16, 8, device=gpu)
+    e.reset()
+    with pytest.raises(_lib.StencilError):
+        e.sweep(e.a, e.b, -1, 8)
 
 
 def test_fused_needs_deep_halo(gpu):

@@ -74,13 +74,14 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, outdir, iterations, depth, fused, init):
+def _worker(rank, world, port, outdir, iterations, depth, fused, init, split2=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, count = partition(NZ, world, rank)
     be = OracleSlabBackend(count, depth, rank > 0, rank < world - 1, fused)
     slab = SlabJacobi(be, SlabInfo(rank, world, first, count), TorchDistExchanger(rank, world))
+    slab.split2 = split2
     slab.init(init, seed=31, plane_elems=NX * NY)
     slab.run(iterations)
     g = be._np(slab.cur)
@@ -91,13 +92,16 @@ def _worker(rank, world, port, outdir, iterations, depth, fused, init):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("depth,fused", [(1, False), (2, False), (2, True)])
+@pytest.mark.parametrize("depth,fused,split2", [(1, False, True), (2, False, False), (2, False, True),
+                                                (2, True, False)])
 @pytest.mark.parametrize("iterations", [4, 5])
-def test_slab_matches_single_process(world, depth, fused, iterations):
+def test_slab_matches_single_process(world, depth, fused, split2, iterations):
+    """single sweeps (depth 1 or 2), split2 rounds (two single sweeps per
+    2-plane exchange) and fused rounds, each bitwise equal to one process."""
     p = ob.problem(3, "fp64", "star", 1, "naive", NX, NY, NZ)
     want = ob.interior(p, ob.run(p, iterations, "random", 31))
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, _free_port(), d, iterations, depth, fused, "random"),
+        mp.start_processes(_worker, args=(world, _free_port(), d, iterations, depth, fused, "random", split2),
                            nprocs=world, join=True, start_method="fork")
         got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)], axis=0)
     assert got.shape == want.shape
