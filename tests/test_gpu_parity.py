@@ -204,6 +204,30 @@ def test_full_size_c2_1000_iterations_properties(gpu):
     assert torch.equal(e2.interior(fin2), inner)
 
 
+@pytest.mark.parametrize("cfg", ["C5_slab_box_fp64", "C4_slab_fp64", "C3_fp32_4096sq"])
+def test_full_size_baseline_configs(gpu, cfg):
+    """Per-GPU shapes of BASELINE configs 3-5 at full x/y size, bitwise
+    against the multithreaded oracle for a few sweeps (the oracle cannot run
+    the full iteration counts in test time):
+      C5: one GPU's slab of 2048^3 27-point (2048^2 x 256), 3 sweeps
+      C4: one GPU's slab of 2048^2 x 4096 7-point, 2048^2 x 64 planes, 4 sweeps
+      C3: 4096^2 x 32 fp32 7-point (4096^3 does not fit), 4 sweeps (fused pairs)"""
+    import torch
+    shapes = {"C5_slab_box_fp64": ("box", "fp64", (2048, 2048, 256), 3),
+              "C4_slab_fp64": ("star", "fp64", (2048, 2048, 64), 4),
+              "C3_fp32_4096sq": ("star", "fp32", (4096, 4096, 32), 4)}
+    shape, dtype, (nx, ny, nz), it = shapes[cfg]
+    p = ob.problem(3, dtype, shape, 1, "naive", nx, ny, nz)
+    want = ob.interior(p, ob.run(p, it, "random", 2025, threads=16))
+    e = engine(gpu, 3, dtype, shape, 1, "naive", "auto", nx, ny, nz)
+    e.reset("random", 2025)
+    fin, _ = e.iterate(it)
+    got = e.interior(fin).cpu().numpy()
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
+    del e
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------- reference-compatible entry points
 @pytest.mark.parametrize("fn,order", [("stencil_iterate_dma", "dma"), ("stencil_iterate_dma_static_unroll", "naive"),
                                       ("stencil_iterate_dma_slave_pack", "dma"), ("stencil_iterate_rma", "dma")])
