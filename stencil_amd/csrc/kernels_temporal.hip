@@ -39,6 +39,11 @@ struct Vec {
 };
 
 template <typename T, int V, int RY, int NW>
+struct T2Tile;
+
+__device__ __forceinline__ bool ld_ok_guard(bool b) { return b; }
+
+template <typename T, int V, int RY, int NW>
 struct T2Tile {
     static constexpr int RW = 64 * V;      // region width
     static constexpr int TX = RW - 2 * V;  // output tile width
@@ -234,12 +239,202 @@ __global__ void __launch_bounds__(64 * NW)
     }
 }
 
+// Variant: centre values come back from LDS instead of register rings.  A
+// thread re-reads ITS OWN cells of in(p-2), in(p-1), t1(p-2) and t1(p-3) from
+// the LDS buffers that still hold them (only the owner writes those words, so
+// no extra barrier), which frees the t1 ring and most of the input ring; the
+// freed VGPRs buy a deeper load lead: plane p+R-1 is requested at iteration p
+// (R-1 iterations before first use) as soon as in(p-1) has been staged.
+template <typename T, int V, int RY, int NW, int R>
+__global__ void __launch_bounds__(64 * NW)
+    temporal2_7pt_lc(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
+                     int zchunk, int tiles_x, int tiles_y, int tiles_z, int64_t t1_lo, int64_t t1_hi,
+                     int64_t ld_lo, int64_t ld_hi, T avg) {
+    using Tl = T2Tile<T, V, RY, NW>;
+    using VT = typename Vec<T, V>::type;
+    constexpr int TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
+    __shared__ __attribute__((aligned(16))) T lin[2][LY][LX];
+    __shared__ __attribute__((aligned(16))) T lt1[2][LY][LX];
+    static_assert(R % 2 == 0 && R >= 4, "ring size must be even and >= 4");
+
+    const int nb = tiles_x * tiles_y * tiles_z;
+    int t = blockIdx.x;
+    if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
+    const int bx = t % tiles_x;
+    const int by = (t / tiles_x) % tiles_y;
+    const int bz = t / (tiles_x * tiles_y);
+
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x0 = int64_t(bx) * TX, y0 = int64_t(by) * TY;
+    const int64_t x = x0 - V + int64_t(lane) * V;
+    const int64_t za = zbeg + int64_t(bz) * zchunk;
+    const int64_t zb = za + zchunk < zend ? za + zchunk : zend;
+    const T* __restrict__ src = in + g.origin;
+    T* __restrict__ dst = out + g.origin;
+    const int64_t plane = g.plane;
+
+    {
+        const int tid = threadIdx.y * 64 + threadIdx.x;
+        constexpr int NPAD = 2 * LX + (LY - 2) * 2 * V;
+        for (int i = tid; i < NPAD; i += 64 * NW) {
+            int rr, cc;
+            if (i < 2 * LX) {
+                rr = i < LX ? 0 : LY - 1;
+                cc = i % LX;
+            } else {
+                const int j = i - 2 * LX;
+                rr = 1 + j / (2 * V);
+                const int c = j % (2 * V);
+                cc = c < V ? c : Tl::RW + c;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                lin[b][rr][cc] = T(0);
+                lt1[b][rr][cc] = T(0);
+            }
+        }
+    }
+
+    int64_t off[RY];
+    bool ldok[RY], yin[RY], st[RY];
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int rr = w + NW * k;
+        const int64_t y = y0 - 2 + rr;
+        off[k] = y * g.row + x;
+        ldok[k] = y >= -1 && y <= g.ny && x <= g.nx;
+        yin[k] = y >= 0 && y < g.ny;
+        st[k] = rr >= 2 && rr < RH - 2 && y < g.ny && lane >= 1 && lane <= 62;
+    }
+    bool xin[V], xst[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        xin[j] = x + j >= 0 && x + j < g.nx;
+        xst[j] = x + j < g.nx;
+    }
+    const int64_t zlast = zb + 1 < ld_hi ? zb + 1 : ld_hi;
+
+    // slot of plane q = (q - za + 1) mod R: slot 0 holds in(za-1); plane
+    // p-1+R is requested at iteration p and first used at iteration p+R-1
+    VT vin[R][RY];
+#pragma unroll
+    for (int s2 = 0; s2 < R; ++s2)
+#pragma unroll
+        for (int k = 0; k < RY; ++k) vin[s2][k] = VT{};
+
+    auto load_plane = [&](VT (&d)[RY], int64_t z) {
+        if (z >= ld_lo && z <= zlast) {
+#pragma unroll
+            for (int k = 0; k < RY; ++k)
+                if (ld_ok_guard(ldok[k])) d[k] = *reinterpret_cast<const VT*>(src + z * plane + off[k]);
+        }
+    };
+
+    // in(za-2) goes straight to LDS buffer 1 (it is read at iteration za as in(p-2))
+    {
+        VT tmp[RY];
+#pragma unroll
+        for (int k = 0; k < RY; ++k) tmp[k] = VT{};
+        load_plane(tmp, za - 2);
+#pragma unroll
+        for (int k = 0; k < RY; ++k)
+            *reinterpret_cast<VT*>(&lin[1][w + NW * k + 1][V + lane * V]) = tmp[k];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) load_plane(vin[i], za - 1 + i);
+    __syncthreads();
+
+    auto step = [&](auto S_, int64_t p) {
+        constexpr int S = decltype(S_)::value;
+        constexpr int IM1 = S, I0 = (S + 1) % R;  // slots of in(p-1), in(p)
+        constexpr int B = S & 1, BP = B ^ 1;
+        const int xx = V + lane * V;
+        // 1. stage in(p-1); its register slot is free again: request plane p-1+R
+#pragma unroll
+        for (int k = 0; k < RY; ++k) *reinterpret_cast<VT*>(&lin[B][w + NW * k + 1][xx]) = vin[IM1][k];
+        load_plane(vin[IM1], p - 1 + R);
+        __syncthreads();
+        const int64_t z1 = p - 1;
+        const bool zin1 = z1 >= t1_lo && z1 < t1_hi;
+        const bool do2 = p - 2 >= za;
+#pragma unroll
+        for (int k = 0; k < RY; ++k) {
+            const int yy = w + NW * k + 1;
+            // own centres still in LDS
+            const VT c = *reinterpret_cast<const VT*>(&lin[B][yy][xx]);    // in(p-1)
+            const VT zm = *reinterpret_cast<const VT*>(&lin[BP][yy][xx]);  // in(p-2)
+            const VT t3 = *reinterpret_cast<const VT*>(&lt1[B][yy][xx]);   // t1(p-3)
+            const VT up = *reinterpret_cast<const VT*>(&lin[B][yy - 1][xx]);
+            const VT dn = *reinterpret_cast<const VT*>(&lin[B][yy + 1][xx]);
+            const T wl = lin[B][yy][xx - 1], er = lin[B][yy][xx + V];
+            const VT zp = vin[I0][k];
+            VT o;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                T s = T(0);
+                s += j == 0 ? wl : c[j - 1];
+                s += j == V - 1 ? er : c[j + 1];
+                s += up[j];
+                s += dn[j];
+                s += zm[j];
+                s += zp[j];
+                o[j] = (zin1 && yin[k] && xin[j]) ? s * avg : c[j];
+            }
+            *reinterpret_cast<VT*>(&lt1[B][yy][xx]) = o;  // t1(p-1) replaces t1(p-3)
+            if (do2) {
+                const T* cr = &lt1[BP][yy][xx];
+                const VT c2 = *reinterpret_cast<const VT*>(cr);  // t1(p-2)
+                const VT up2 = *reinterpret_cast<const VT*>(&lt1[BP][yy - 1][xx]);
+                const VT dn2 = *reinterpret_cast<const VT*>(&lt1[BP][yy + 1][xx]);
+                const T wl2 = cr[-1], er2 = cr[V];
+                VT o2;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    T s = T(0);
+                    s += j == 0 ? wl2 : c2[j - 1];
+                    s += j == V - 1 ? er2 : c2[j + 1];
+                    s += up2[j];
+                    s += dn2[j];
+                    s += t3[j];
+                    s += o[j];
+                    o2[j] = s * avg;
+                }
+                if (st[k]) {
+                    T* q = dst + (p - 2) * plane + off[k];
+                    if (xst[V - 1]) {
+                        __builtin_nontemporal_store(o2, reinterpret_cast<VT*>(q));
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < V; ++j)
+                            if (xst[j]) q[j] = o2[j];
+                    }
+                }
+            }
+        }
+    };
+
+    for (int64_t p = za; p <= zb + 1; p += R) {
+        step(std::integral_constant<int, 0>{}, p);
+        if (p + 1 <= zb + 1) step(std::integral_constant<int, 1>{}, p + 1);
+        if (p + 2 <= zb + 1) step(std::integral_constant<int, 2>{}, p + 2);
+        if (p + 3 <= zb + 1) step(std::integral_constant<int, 3>{}, p + 3);
+        if constexpr (R > 4) {
+            if (p + 4 <= zb + 1) step(std::integral_constant<int, 4 % R>{}, p + 4);
+            if (p + 5 <= zb + 1) step(std::integral_constant<int, 5 % R>{}, p + 5);
+        }
+        if constexpr (R > 6) {
+            if (p + 6 <= zb + 1) step(std::integral_constant<int, 6 % R>{}, p + 6);
+            if (p + 7 <= zb + 1) step(std::integral_constant<int, 7 % R>{}, p + 7);
+        }
+    }
+}
+
 int env_int(const char* name, int dflt) {
     const char* s = std::getenv(name);
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int R = 4>
+template <typename T, int V, int RY, int NW, int R = 4, bool LC = false>
 int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
               hipStream_t s) {
     using Tl = T2Tile<T, V, RY, NW>;
@@ -264,9 +459,14 @@ int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin,
         return set_error(STENCIL_EINVAL, "fused steps across a slab halo need halo >= 2 (got %lld)", (long long)l.zghost);
     const int64_t t1_lo = lo ? -1 : 0, t1_hi = hi ? g.nz + 1 : g.nz;
     const int64_t ld_lo = lo ? -2 : -1, ld_hi = hi ? g.nz + 1 : g.nz;
-    hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW, R>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
-                       static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
+    if constexpr (LC)
+        hipLaunchKernelGGL((temporal2_7pt_lc<T, V, RY, NW, R>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
+                           int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
+    else
+        hipLaunchKernelGGL((temporal2_7pt<T, V, RY, NW, R>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
+                           int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
@@ -295,6 +495,10 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
     case 48: return launch_t2<double, 2, 4, 8>(l, in, out, begin, end, s);
     case 28: return launch_t2<double, 2, 2, 8>(l, in, out, begin, end, s);
     case 84: return launch_t2<double, 2, 8, 4>(l, in, out, begin, end, s);
+    case 1004: return launch_t2<double, 2, 2, 16, 4, true>(l, in, out, begin, end, s);
+    case 1006: return launch_t2<double, 2, 2, 16, 6, true>(l, in, out, begin, end, s);
+    case 1008: return launch_t2<double, 2, 2, 16, 8, true>(l, in, out, begin, end, s);
+    case 1046: return launch_t2<double, 2, 4, 8, 6, true>(l, in, out, begin, end, s);
     default: return launch_t2<double, 2, 2, 16>(l, in, out, begin, end, s);
     }
 }
