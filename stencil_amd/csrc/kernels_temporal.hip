@@ -488,6 +488,7 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
         switch (cfg) {
         case 48: return launch_t2<float, 4, 4, 8>(l, in, out, begin, end, s);
         case 28: return launch_t2<float, 4, 2, 8>(l, in, out, begin, end, s);
+        case 1004: return launch_t2<float, 4, 2, 16, 4, true>(l, in, out, begin, end, s);
         default: return launch_t2<float, 4, 2, 16>(l, in, out, begin, end, s);
         }
     }
@@ -499,6 +500,9 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
     case 1006: return launch_t2<double, 2, 2, 16, 6, true>(l, in, out, begin, end, s);
     case 1008: return launch_t2<double, 2, 2, 16, 8, true>(l, in, out, begin, end, s);
     case 1046: return launch_t2<double, 2, 4, 8, 6, true>(l, in, out, begin, end, s);
+    case 1044: return launch_t2<double, 2, 4, 8, 4, true>(l, in, out, begin, end, s);
+    case 1312: return launch_t2<double, 2, 3, 12, 4, true>(l, in, out, begin, end, s);
+    case 1310: return launch_t2<double, 2, 3, 10, 4, true>(l, in, out, begin, end, s);
     default: return launch_t2<double, 2, 2, 16>(l, in, out, begin, end, s);
     }
 }
