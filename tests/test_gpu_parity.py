@@ -107,12 +107,16 @@ def test_3d_r1_random_ragged(gpu, stencil, dtype, kernel, shape3):
         assert same_bits(got, want), (it, shape3)
 
 
+@pytest.mark.parametrize("t2cfg", ["default", "216", "1312"])
 @pytest.mark.parametrize("zchunk", ["8", "9", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("stencil", ["star", "box"])
-def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype, stencil):
+def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype, stencil, t2cfg):
     """Fused two-step launches with forced z-chunk sizes (chunk seams,
-    remainder chunks), odd iteration counts (a trailing single sweep)."""
+    remainder chunks), odd iteration counts (a trailing single sweep), for the
+    default LDS-centre kernel and the register-ring shapes kept for A/B."""
+    if t2cfg != "default":
+        monkeypatch.setenv("STENCIL_T2_CFG", t2cfg)
     monkeypatch.setenv("STENCIL_T2_ZCHUNK", zchunk)
     monkeypatch.setenv("STENCIL_BOX_ZCHUNK", zchunk)
     nx, ny, nz = 131, 61, 29
