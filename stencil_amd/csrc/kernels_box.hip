@@ -46,7 +46,7 @@ template <typename T, int V, int RY, int NW, int STEPS>
 __global__ void __launch_bounds__(64 * NW)
     box27_zmarch(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
                  int zchunk, int tiles_x, int tiles_y, int tiles_z, int64_t t1_lo, int64_t t1_hi,
-                 int64_t ld_lo, int64_t ld_hi, T avg) {
+                 int64_t ld_lo, int64_t ld_hi, int remap, T avg) {
     using Tl = BoxTile<T, V, RY, NW, STEPS>;
     using VT = typename BVec<T, V>::type;
     constexpr int TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY, RW = Tl::RW;
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(64 * NW)
 
     const int nb = tiles_x * tiles_y * tiles_z;
     int t = blockIdx.x;
-    if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
+    if (remap && (nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
     const int bx = t % tiles_x;
     const int by = (t / tiles_x) % tiles_y;
     const int bz = t / (tiles_x * tiles_y);
@@ -308,7 +308,8 @@ int launch_box(const stencil_layout& l, const void* in, void* out, int64_t begin
     }
     hipLaunchKernelGGL((box27_zmarch<T, V, RY, NW, STEPS>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, avg_weight<T>(l.prob));
+                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, env_int("STENCIL_BOX_REMAP", 1),
+                       avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }

@@ -51,7 +51,7 @@ struct ZTile {
 template <typename T, int V, int RY>
 __global__ void __launch_bounds__(64 * kBY)
     zmarch7(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
-            int zchunk, int tiles_x, int tiles_y, int tiles_z, T avg) {
+            int zchunk, int tiles_x, int tiles_y, int tiles_z, int remap, T avg) {
     using Tile = ZTile<T, V, RY>;
     using VT = typename Vec<T, V>::type;
     constexpr int TX = Tile::TX, TY = Tile::TY, LX = Tile::LX, LY = Tile::LY;
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(64 * kBY)
     // ---- XCD-aware tile order (speed only) ----
     const int nb = tiles_x * tiles_y * tiles_z;
     int t = blockIdx.x;
-    if ((nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
+    if (remap && (nb & 7) == 0) t = (t & 7) * (nb >> 3) + (t >> 3);
     const int bx = t % tiles_x;
     const int by = (t / tiles_x) % tiles_y;
     const int bz = t / (tiles_x * tiles_y);
@@ -228,7 +228,7 @@ int launch_zm(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for zmarch");
     hipLaunchKernelGGL((zmarch7<T, V, RY>), dim3(unsigned(nb)), dim3(64, kBY, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), avg_weight<T>(l.prob));
+                       int(gy), int(gz), env_int("STENCIL_ZM_REMAP", 1), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
