@@ -308,7 +308,7 @@ int launch_box(const stencil_layout& l, const void* in, void* out, int64_t begin
     }
     hipLaunchKernelGGL((box27_zmarch<T, V, RY, NW, STEPS>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, env_int("STENCIL_BOX_REMAP", 1),
+                       int(gy), int(gz), t1_lo, t1_hi, ld_lo, ld_hi, env_int("STENCIL_BOX_REMAP", 0),
                        avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;

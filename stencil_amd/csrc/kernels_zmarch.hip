@@ -228,7 +228,7 @@ int launch_zm(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for zmarch");
     hipLaunchKernelGGL((zmarch7<T, V, RY>), dim3(unsigned(nb)), dim3(64, kBY, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx),
-                       int(gy), int(gz), env_int("STENCIL_ZM_REMAP", 1), avg_weight<T>(l.prob));
+                       int(gy), int(gz), env_int("STENCIL_ZM_REMAP", 0), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
