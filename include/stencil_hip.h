@@ -95,7 +95,9 @@ enum {
     STENCIL_KERNEL_AUTO = 0,
     STENCIL_KERNEL_DIRECT = 1,    /* one cell per lane, neighbours via L1/L2 */
     STENCIL_KERNEL_ZMARCH = 2,    /* 2.5D: LDS plane + z register queue */
-    STENCIL_KERNEL_TEMPORAL2 = 3  /* ZMARCH with 2 fused time steps per launch */
+    STENCIL_KERNEL_TEMPORAL2 = 3, /* ZMARCH with 2 fused time steps per launch */
+    STENCIL_KERNEL_TEMPORALK = 4  /* 3D 7-point star: K = 3 or 4 fused steps per launch
+                                     (K = env STENCIL_TK_STEPS, default 3) */
 };
 enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
 /* stencil_problem.flags: which z faces of this grid are halos filled by a
@@ -175,10 +177,17 @@ int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t be
 int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
                    void* stream);
 
+/* K fused sweeps, out = S^K(in) on [begin, end): steps 1 = stencil_sweep,
+ * 2 = stencil_sweep2, 3 or 4 = the TEMPORALK kernel (3D 7-point star only).
+ * With HALO_LO/HI flags the grid needs halo >= steps. */
+int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                   int32_t steps, void* stream);
+
 /* Whole job: `iterations` ping-pong sweeps starting from grid `a` (grid `b`
  * must hold the same ghosts). *final_in_b = 1 when the result is in `b`
  * (iterations odd), 0 when in `a` (parity rule, stencil.cpp:88-92,134).
- * With prob.kernel == TEMPORAL2, pairs of iterations run as one launch.
+ * With prob.kernel == TEMPORAL2, pairs of iterations run as one launch;
+ * with TEMPORALK, K-tuples (remainder as a pair and/or a single sweep).
  * If elapsed_ms is non-NULL the call brackets its launches with hipEvents on
  * `stream`, synchronises, and stores the elapsed device time. */
 int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iterations, void* stream,

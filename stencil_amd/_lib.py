@@ -17,11 +17,12 @@ STENCIL_OK = 0
 F32, F64 = 0, 1
 STAR, BOX = 0, 1
 ORDER_NAIVE, ORDER_DMA = 0, 1
-KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2 = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2, KERNEL_TEMPORALK = 0, 1, 2, 3, 4
 INIT_REFERENCE, INIT_RANDOM = 0, 1
 HALO_LO, HALO_HI = 1, 2
 
-KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2}
+KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2,
+                "temporalk": KERNEL_TEMPORALK}
 
 # Every symbol include/stencil_hip.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -30,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "stencil_iterate_rma",
     "stencil_layout_init", "stencil_slow_extent", "stencil_device_count", "stencil_set_device",
     "stencil_synchronize", "stencil_alloc", "stencil_free", "stencil_fill_initial", "stencil_upload",
-    "stencil_download", "stencil_copy_planes", "stencil_sweep", "stencil_sweep2", "stencil_iterate",
+    "stencil_download", "stencil_copy_planes", "stencil_sweep", "stencil_sweep2", "stencil_sweepk", "stencil_iterate",
     "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth",
 )
 
@@ -97,6 +98,7 @@ def load() -> ctypes.CDLL:
         "stencil_copy_planes": (c_int, [L, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p]),
         "stencil_sweep": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
         "stencil_sweep2": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+        "stencil_sweepk": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
         "stencil_iterate": (c_int, [L, c_void_p, c_void_p, c_uint32, c_void_p, POINTER(c_int), POINTER(c_float)]),
         "stencil_plan": (c_int, [L, c_uint32, POINTER(c_int64), POINTER(c_int32)]),
         "stencil_plane_sums": (c_int, [L, c_void_p, POINTER(c_double), c_void_p]),

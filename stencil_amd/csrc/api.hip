@@ -47,7 +47,7 @@ int check_problem(const stencil_problem* p) {
     if (p->order != STENCIL_ORDER_NAIVE && p->order != STENCIL_ORDER_DMA) return set_error(STENCIL_EINVAL, "bad order %d", p->order);
     if (p->order == STENCIL_ORDER_DMA && (p->dims != 2 || p->shape != STENCIL_STAR))
         return set_error(STENCIL_EINVAL, "DMA sum order is defined for 2D star stencils only");
-    if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_TEMPORAL2) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
+    if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_TEMPORALK) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
     if (p->nx < 0 || p->ny < 0 || p->nz < 0) return set_error(STENCIL_EINVAL, "negative extent");
     if (p->dims == 2 && p->nz != 1) return set_error(STENCIL_EINVAL, "2D problems need nz = 1");
     if (p->halo < 0 || (p->halo > 0 && p->halo < p->radius) || p->halo > 64)
@@ -59,6 +59,8 @@ int check_problem(const stencil_problem* p) {
     if (p->kernel == STENCIL_KERNEL_TEMPORAL2 && !fused_supported(*p) && !tb2d_supports(*p))
         return set_error(STENCIL_EUNSUPPORTED,
                          "TEMPORAL2 kernels cover 3D r=1 naive star/box and 2D star r<=4 only");
+    if (p->kernel == STENCIL_KERNEL_TEMPORALK && !temporal2_supports(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "TEMPORALK kernels cover the 3D r=1 naive 7-point star only");
     return STENCIL_OK;
 }
 
@@ -77,12 +79,30 @@ int sweep_family(const stencil_problem& p) {
 // Does stencil_iterate fuse pairs of sweeps?  Explicit TEMPORAL2, or AUTO on
 // a problem a fused kernel supports (STENCIL_NO_T2=1 disables the latter).
 bool iterate_fused(const stencil_problem& p) {
-    if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
+    if (p.kernel == STENCIL_KERNEL_TEMPORAL2 || p.kernel == STENCIL_KERNEL_TEMPORALK) return true;
     // AUTO fuses the 7-point star only: the fused 27-point kernel is slower
     // than its single sweep on MI355X.
     if (p.kernel != STENCIL_KERNEL_AUTO || !temporal2_supports(p)) return false;
     const char* e = std::getenv("STENCIL_NO_T2");
     return !(e && *e && *e != '0');
+}
+
+// Steps per launch of the deep temporal-blocking family (kernels_temporalk.hip)
+// in stencil_iterate: K = STENCIL_TK_STEPS (3 or 4, default 3) for explicit
+// TEMPORALK and for AUTO on the 7-point star (STENCIL_NO_TK=1 or
+// STENCIL_NO_T2=1 turn the latter off); 0 = not used.
+int iterate_tk_steps(const stencil_problem& p) {
+    if (!temporal2_supports(p)) return 0;
+    if (p.kernel == STENCIL_KERNEL_AUTO) {
+        if (!iterate_fused(p)) return 0;
+        const char* e = std::getenv("STENCIL_NO_TK");
+        if (e && *e && *e != '0') return 0;
+    } else if (p.kernel != STENCIL_KERNEL_TEMPORALK) {
+        return 0;
+    }
+    const char* k = std::getenv("STENCIL_TK_STEPS");
+    const int steps = k && *k ? std::atoi(k) : 3;
+    return steps == 3 || steps == 4 ? steps : 0;
 }
 
 // 2D problems iterate K sweeps per launch with the tile resident in LDS
@@ -368,6 +388,22 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
     return rc;
 }
 
+int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end, int32_t steps,
+                   void* stream) {
+    if (steps == 1) return stencil_sweep(l, in, out, begin, end, stream);
+    if (steps == 2) return stencil_sweep2(l, in, out, begin, end, stream);
+    if (int rc = check_layout(l)) return rc;
+    if (steps != 3 && steps != 4) return set_error(STENCIL_EINVAL, "steps must be 1..4 (got %d)", steps);
+    if (!temporal2_supports(l->prob))
+        return set_error(STENCIL_EUNSUPPORTED, "3- and 4-step fused sweeps cover the 3D r=1 naive 7-point star only");
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range out of bounds");
+    if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
+    const int rc = launch_temporalk(*l, in, out, begin, end, steps, as_stream(stream));
+    if (rc == STENCIL_OK) clear_error();
+    return rc;
+}
+
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {
     if (int rc = check_layout(l)) return rc;
     if (iterate_tb2d(l->prob)) {
@@ -377,8 +413,16 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
         return STENCIL_OK;
     }
     const bool t2 = !iterate_tb2d(l->prob) && iterate_fused(l->prob);
-    if (launches) *launches = t2 ? int64_t(iterations / 2 + iterations % 2) : int64_t(iterations);
-    if (kernel) *kernel = t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
+    const int64_t k = iterate_tk_steps(l->prob);
+    int64_t n = iterations;
+    if (k) {
+        const int64_t r = n % k;
+        n = n / k + r / 2 + r % 2;
+    } else if (t2) {
+        n = n / 2 + n % 2;
+    }
+    if (launches) *launches = n;
+    if (kernel) *kernel = k ? STENCIL_KERNEL_TEMPORALK : t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
     return STENCIL_OK;
 }
 
@@ -406,6 +450,12 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
             rc = launch_tb2d(*l, in, out, int(n2), s);
             std::swap(in, out);
             i += n2;
+        }
+    }
+    if (const uint32_t k = uint32_t(iterate_tk_steps(l->prob))) {
+        for (; i + k <= iterations && rc == STENCIL_OK; i += k) {
+            rc = launch_temporalk(*l, in, out, 0, n, int(k), s);
+            std::swap(in, out);
         }
     }
     if (t2) {

@@ -22,6 +22,7 @@ int kernel_of(const std::string& k) {
     if (k == "direct") return STENCIL_KERNEL_DIRECT;
     if (k == "zmarch") return STENCIL_KERNEL_ZMARCH;
     if (k == "temporal2") return STENCIL_KERNEL_TEMPORAL2;
+    if (k == "temporalk") return STENCIL_KERNEL_TEMPORALK;
     return STENCIL_KERNEL_AUTO;
 }
 
@@ -92,6 +93,7 @@ auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGri
     case HIP_DIRECT: p.kernel = STENCIL_KERNEL_DIRECT; break;
     case HIP_ZMARCH: p.kernel = STENCIL_KERNEL_ZMARCH; break;
     case HIP_TEMPORAL2: p.kernel = STENCIL_KERNEL_TEMPORAL2; break;
+    case HIP_TEMPORALK: p.kernel = STENCIL_KERNEL_TEMPORALK; break;
     case HIP: p.kernel = kernel_of(options.kernel); break;
     default: p.kernel = STENCIL_KERNEL_AUTO; break;
     }
@@ -152,6 +154,7 @@ auto Stencil::run(std::string_view method_name) -> std::optional<std::chrono::st
         {"HIPDirect", HIP_DIRECT},
         {"HIPZMarch", HIP_ZMARCH},
         {"HIPTemporal2", HIP_TEMPORAL2},
+        {"HIPTemporalK", HIP_TEMPORALK},
     };
     auto const iter = method_map.find(method_name);
     if (iter == method_map.end()) return std::nullopt;

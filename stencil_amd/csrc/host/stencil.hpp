@@ -29,6 +29,7 @@ public:
         HIP_DIRECT,         ///< naive order, general one-cell-per-lane kernel
         HIP_ZMARCH,         ///< naive order, 2.5D LDS/register z-marching kernel (3D r=1)
         HIP_TEMPORAL2,      ///< naive order, two fused time steps per launch
+        HIP_TEMPORALK,      ///< naive order, 3 or 4 fused time steps per launch (7-point star)
     };
 
     Stencil() = default;

@@ -29,7 +29,7 @@ class StencilSpec:
     shape: str = "star"          # "star" | "box"
     radius: int = 1
     order: str = "naive"         # "naive" | "dma"
-    kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2"
+    kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2" | "temporalk"
     halo: int = 0                # 3D ghost planes per z side (0 = radius); 2 for fused slabs
 
     def problem(self, nx: int, ny: int, nz: int, flags: int = 0) -> _lib.Problem:
@@ -46,7 +46,7 @@ class StencilSpec:
         if self.dims != 3 or self.radius != 1 or self.order != "naive":
             return False
         # the fused 27-point kernel is slower than its single sweep: explicit only
-        return self.kernel == "temporal2" or (self.kernel == "auto" and self.shape == "star")
+        return self.kernel in ("temporal2", "temporalk") or (self.kernel == "auto" and self.shape == "star")
 
     @property
     def elem_bytes(self) -> int:
@@ -103,6 +103,12 @@ class JacobiEngine:
         _lib.check(self.lib.stencil_sweep2(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, _stream_handle(stream)),
                    "stencil_sweep2")
+
+    def sweepk(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int, stream=None) -> None:
+        """dst = S^steps(src) on [begin, end) in one launch (steps 1..4)."""
+        _lib.check(self.lib.stencil_sweepk(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
+                                           ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
+                                           _stream_handle(stream)), "stencil_sweepk")
 
     def iterate(self, iterations: int, stream=None, timed: bool = False):
         """Whole job a -> ... ; returns (final grid tensor, device ms or None)."""

@@ -105,7 +105,7 @@ def test_error_strings():
         _lib.make_layout(_lib.make_problem(dims=2, radius=0, nx=4, ny=4))
 
 
-def test_plan_counts_launches():
+def test_plan_counts_launches(monkeypatch):
     lib = _lib.load()
     lay2 = _lib.make_layout(_lib.make_problem(dims=2, nx=64, ny=64))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
@@ -114,7 +114,15 @@ def test_plan_counts_launches():
     lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
-    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # AUTO fuses pairs
+    assert launches.value == 3 and kernel.value == _lib.KERNEL_TEMPORALK  # AUTO: 3 + 3 fused, 1 single
+    monkeypatch.setenv("STENCIL_TK_STEPS", "4")
+    assert lib.stencil_plan(ctypes.byref(lay), 11, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORALK  # 4 + 4 + pair + single
+    monkeypatch.setenv("STENCIL_NO_TK", "1")
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # pairs + single
+    monkeypatch.delenv("STENCIL_NO_TK")
+    monkeypatch.delenv("STENCIL_TK_STEPS")
     lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8, kernel=_lib.KERNEL_ZMARCH))
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_ZMARCH

@@ -94,14 +94,16 @@ def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype):
 # ------------------------------------------------------- 3D hot kernels
 @pytest.mark.parametrize("stencil", ["star", "box"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("kernel", ["direct", "zmarch", "temporal2"])
+@pytest.mark.parametrize("kernel", ["direct", "zmarch", "temporal2", "temporalk"])
 @pytest.mark.parametrize("shape3", [(64, 16, 8), (130, 37, 29), (1, 1, 1), (65, 17, 3), (200, 3, 70), (124, 28, 2),
                                     (249, 57, 11)])
 def test_3d_r1_random_ragged(gpu, stencil, dtype, kernel, shape3):
     """7-point star and 27-point box, r = 1, every kernel family."""
+    if kernel == "temporalk" and stencil == "box":
+        pytest.skip("TEMPORALK is the 7-point star family")
     nx, ny, nz = shape3
     p = ob.problem(3, dtype, stencil, 1, "naive", nx, ny, nz)
-    for it in (1, 2, 5):
+    for it in (1, 2, 5, 7):
         want = ob.run(p, it, "random", 1234 + it)
         _, got = gpu_run(gpu, 3, dtype, stencil, 1, "naive", kernel, nx, ny, nz, it, "random", 1234 + it)
         assert same_bits(got, want), (it, shape3)
@@ -125,6 +127,55 @@ def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype, stencil, t2cfg):
         want = ob.run(p, it, "random", 99 + it)
         _, got = gpu_run(gpu, 3, dtype, stencil, 1, "naive", "temporal2", nx, ny, nz, it, "random", 99 + it)
         assert same_bits(got, want), it
+
+
+@pytest.mark.parametrize("steps,cfg", [("3", "default"), ("3", "312"), ("3", "608"), ("4", "default"),
+                                       ("4", "408")])
+@pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
+    """K = 3 / 4 fused sweeps per launch: every workgroup shape, forced z-chunk
+    sizes (seams, remainder chunks, chunks shorter than the 2K-plane halo) and
+    iteration counts leaving a remainder pair / single sweep."""
+    monkeypatch.setenv("STENCIL_TK_STEPS", steps)
+    monkeypatch.setenv("STENCIL_TK_ZCHUNK", zchunk)
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_TK_CFG", cfg)
+    nx, ny, nz = 131, 61, 29
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    for it in (3, 4, 5, 9):
+        want = ob.run(p, it, "random", 7 + it)
+        e, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", "temporalk", nx, ny, nz, it, "random", 7 + it)
+        assert same_bits(got, want), it
+    k = int(steps)
+    assert e.plan(9) == (9 // k + (9 % k) // 2 + (9 % k) % 2, 4)
+
+
+@pytest.mark.parametrize("steps", [3, 4])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_temporalk_signed_zero_field(gpu, steps, dtype):
+    """The K-step kernel folds the reference's leading `0 +` into
+    fma(sum, avg, +0); a block of -0.0 cells (where 0 + -0 = +0 matters) and
+    mixed-sign data must still match plain sweeps bit for bit."""
+    import torch
+    nx, ny, nz = 77, 40, 23
+    e = engine(gpu, 3, dtype, "star", 1, "naive", "temporalk", nx, ny, nz)
+    e.reset("random", 11)
+    full = e.with_ghosts(e.a)
+    inner = e.interior(e.a)
+    inner[3:15, 5:30, 10:60] = -0.0
+    inner[15:20] *= -1.0
+    torch.cuda.synchronize()
+    start = full.cpu().numpy().copy()
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    a, b = start.copy(), start.copy()
+    for _ in range(steps):
+        ob.sweep(p, a, b, 0, nz)
+        a, b = b, a
+    e.sweepk(e.a, e.b, 0, nz, steps)
+    torch.cuda.synchronize()
+    got = e.with_ghosts(e.b).cpu().numpy()
+    assert same_bits(np.ascontiguousarray(got), np.ascontiguousarray(a))
 
 
 @pytest.mark.parametrize("cfg", ["0"])

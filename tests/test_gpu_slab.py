@@ -16,8 +16,10 @@ from stencil_amd.slab import partition
 pytestmark = pytest.mark.gpu
 
 
-def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star", split2=False):
-    spec = StencilSpec(dims=3, dtype="fp64", halo=2, shape=shape)
+def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star", split2=False, k=2):
+    """`fused`: rounds of k fused sweeps per k-plane exchange (sweepk)."""
+    spec = StencilSpec(dims=3, dtype="fp64", halo=max(2, k), shape=shape)
+    h = spec.halo
     engines, firsts = [], []
     for r in range(world):
         first, count = partition(nz, world, r)
@@ -33,8 +35,8 @@ def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star", sp
         for r in range(world - 1):
             lo, hi = engines[r], engines[r + 1]
             n_lo = firsts[r][1]
-            hi.plane_view(grids[r + 1], -2, 2).copy_(lo.plane_view(grids[r], n_lo - 2, 2))
-            lo.plane_view(grids[r], n_lo, 2).copy_(hi.plane_view(grids[r + 1], 0, 2))
+            hi.plane_view(grids[r + 1], -h, h).copy_(lo.plane_view(grids[r], n_lo - h, h))
+            lo.plane_view(grids[r], n_lo, h).copy_(hi.plane_view(grids[r + 1], 0, h))
 
     exchange(cur)
     done = 0
@@ -49,19 +51,18 @@ def run_slabs(gpu, nx, ny, nz, world, iterations, fused, split, shape="star", sp
             exchange(cur)
             done += 2
     while done < iterations:
-        two = fused and iterations - done >= 2
+        steps = min(k, iterations - done) if fused else 1
         for r, e in enumerate(engines):
             n = firsts[r][1]
-            fn = e.sweep2 if two else e.sweep
-            if split and n > 4:
-                fn(cur[r], nxt[r], 0, 2)
-                fn(cur[r], nxt[r], n - 2, n)
-                fn(cur[r], nxt[r], 2, n - 2)
+            if split and n > 2 * h:
+                e.sweepk(cur[r], nxt[r], 0, h, steps)
+                e.sweepk(cur[r], nxt[r], n - h, n, steps)
+                e.sweepk(cur[r], nxt[r], h, n - h, steps)
             else:
-                fn(cur[r], nxt[r], 0, n)
+                e.sweepk(cur[r], nxt[r], 0, n, steps)
         exchange(nxt)
         cur, nxt = nxt, cur
-        done += 2 if two else 1
+        done += steps
     torch.cuda.synchronize()
     return torch.cat([e.interior(g) for e, g in zip(engines, cur)], dim=0)
 
@@ -78,6 +79,31 @@ def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split, shape):
     want = ref.interior(fin)
     got = run_slabs(gpu, nx, ny, nz, world, it, fused, split, shape)
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("cfg", ["default", "312"])
+def test_slabs_k_step_rounds(gpu, monkeypatch, world, k, split, cfg):
+    """k fused sweeps per k-plane halo exchange (TEMPORALK with HALO_LO/HI):
+    halo planes advanced to t+k-1 .. t+1 inside the launch."""
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_TK_CFG", cfg)
+    monkeypatch.setenv("STENCIL_TK_ZCHUNK", "5")
+    nx, ny, nz, it = 70, 45, 29, 11
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", kernel="direct"), nx, ny, nz, device=gpu)
+    ref.reset("random", 17)
+    fin, _ = ref.iterate(it)
+    got = run_slabs(gpu, nx, ny, nz, world, it, True, split, k=k)
+    assert torch.equal(got, ref.interior(fin))
+
+
+def test_k_step_needs_deep_halo(gpu):
+    e = JacobiEngine(StencilSpec(dims=3, dtype="fp64", halo=2), 16, 16, 8, device=gpu, flags=_lib.HALO_HI)
+    e.reset()
+    with pytest.raises(_lib.StencilError):
+        e.sweepk(e.a, e.b, 0, 8, 3)
 
 
 @pytest.mark.parametrize("shape", ["star", "box"])
