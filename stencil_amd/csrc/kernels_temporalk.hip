@@ -55,6 +55,21 @@ struct VecK {
 __device__ __forceinline__ float fma0(float s, float a) { return __builtin_fmaf(s, a, 0.0f); }
 __device__ __forceinline__ double fma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
 
+// Whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1): lane i receives
+// lane i-1's (shr) or lane i+1's (shl) value; the lane without a source gets 0.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f(double v) {
+    const int2 b = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, b.x, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, b.y, CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
+
 template <typename T, int V, int RY, int NW, int K>
 struct TKTile {
     static constexpr int XR = (K + V - 1) / V;     // ring vectors per x side
@@ -67,7 +82,7 @@ struct TKTile {
     static constexpr size_t lds_bytes = size_t(K) * LY * LX * sizeof(T);
 };
 
-template <typename T, int V, int RY, int NW, int K, int R>
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX>
 __global__ void __launch_bounds__(64 * NW)
     temporalk_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
                   int zchunk, int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
@@ -167,7 +182,14 @@ __global__ void __launch_bounds__(64 * NW)
                 const VT c = *reinterpret_cast<const VT*>(cr);
                 const VT up = *reinterpret_cast<const VT*>(&L[s - 1][yy - 1][xx]);
                 const VT dn = *reinterpret_cast<const VT*>(&L[s - 1][yy + 1][xx]);
-                const T wl = cr[-1], er = cr[V];
+                T wl, er;
+                if constexpr (DPPX) {  // x neighbours from the adjacent lanes' registers
+                    wl = dpp_f<kWaveShr1>(c[V - 1]);
+                    er = dpp_f<kWaveShl1>(c[0]);
+                } else {
+                    wl = cr[-1];
+                    er = cr[V];
+                }
                 const VT zm = hz[P ^ 1][s - 1][k];
                 const VT zp = s == 1 ? vin[S][k] : res[s - 2 < 0 ? 0 : s - 2][k];
                 VT o;
@@ -238,7 +260,7 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, int R>
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false>
 int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
     using Tl = TKTile<T, V, RY, NW, K>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
@@ -246,15 +268,33 @@ int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
+    auto kern = temporalk_7pt<T, V, RY, NW, K, R, DPPX>;
     int zc = env_int("STENCIL_TK_ZCHUNK", 0);
     if (zc <= 0) {
-        // One workgroup per CU fits (LDS), so aim for whole waves of 256
-        // workgroups with chunks long enough to amortise the 2K-plane z halo.
+        // Chunk count c minimising  ceil(tiles*c / slots) * (nz/c + 2K):
+        // workgroups run in "rounds" of `slots` (one per CU here: the LDS
+        // planes take 108 KB), each round costs one chunk march of nz/c + 2K
+        // planes, and a last round that is mostly empty costs as much as a
+        // full one (measured, 512^3 fp64: zc 103 / 52 -> 2 / 3.9 rounds
+        // 885 Gcell/s, zc 64 / 128 -> 3.1 / 1.6 rounds 760-790).
+        static int slots = 0;
+        if (!slots) {
+            int dev = 0, cus = 0, per_cu = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
+                return set_error(STENCIL_EHIP, "occupancy query failed");
+            slots = std::max(1, cus * std::max(1, per_cu));
+        }
         const int64_t tiles = gx * gy;
-        int64_t chunks = std::max<int64_t>(1, (env_int("STENCIL_TK_WG", 1024) + tiles - 1) / tiles);
-        chunks = std::min<int64_t>(chunks, nz);
-        zc = int((nz + chunks - 1) / chunks);
-        zc = std::max(zc, 4);
+        int64_t best_c = 1, best = INT64_MAX;
+        for (int64_t c = 1; c <= nz; ++c) {
+            const int64_t z = (nz + c - 1) / c;
+            if (c > 1 && z < 2 * K) break;  // chunks shorter than their halo
+            const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 2 * K);
+            if (cost <= best) best = cost, best_c = c;
+        }
+        zc = int((nz + best_c - 1) / best_c);
     }
     const int64_t gz = (nz + zc - 1) / zc;
     const int64_t nb = gx * gy * gz;
@@ -263,7 +303,7 @@ int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((lo || hi) && l.zghost < K)
         return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
                          (long long)l.zghost);
-    hipLaunchKernelGGL((temporalk_7pt<T, V, RY, NW, K, R>), dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
+    hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx), int(gy),
                        int(lo), int(hi), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
@@ -276,20 +316,26 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
                      hipStream_t s) {
     if (!temporal2_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "TEMPORALK supports 3D star r=1 naive order only");
-    // cfg = RY*100 + NW: rows per wave x waves (region 64V x RY*NW)
+    // cfg = RY*100 + NW: rows per wave x waves (region 64V x RY*NW); default
+    // x neighbours by DPP lane shifts (+6.6 % fp64 / +13 % fp32 over the LDS
+    // reads of cfg 216, 512^3); 2xxxx / 3xxxx = DPP shapes (3xxxx: fp32, V = 2)
     const int cfg = env_int("STENCIL_TK_CFG", 0);
     if (l.prob.dtype == STENCIL_F32) {
         if (steps == 3) {
             switch (cfg) {
             case 312: return launch_tk<float, 4, 3, 12, 3, 2>(l, in, out, begin, end, s);
             case 608: return launch_tk<float, 4, 6, 8, 3, 2>(l, in, out, begin, end, s);
-            default: return launch_tk<float, 4, 2, 16, 3, 2>(l, in, out, begin, end, s);
+            case 216: return launch_tk<float, 4, 2, 16, 3, 2>(l, in, out, begin, end, s);
+            case 30216: return launch_tk<float, 2, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
+            case 30316: return launch_tk<float, 2, 3, 16, 3, 2, true>(l, in, out, begin, end, s);
+            default: return launch_tk<float, 4, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
             }
         }
         if (steps == 4) {
             switch (cfg) {
             case 408: return launch_tk<float, 4, 4, 8, 4, 2>(l, in, out, begin, end, s);
-            default: return launch_tk<float, 4, 2, 16, 4, 2>(l, in, out, begin, end, s);
+            case 216: return launch_tk<float, 4, 2, 16, 4, 2>(l, in, out, begin, end, s);
+            default: return launch_tk<float, 4, 2, 16, 4, 2, true>(l, in, out, begin, end, s);
             }
         }
     } else {
@@ -297,13 +343,16 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
             switch (cfg) {
             case 312: return launch_tk<double, 2, 3, 12, 3, 2>(l, in, out, begin, end, s);
             case 10216: return launch_tk<double, 2, 2, 16, 3, 4>(l, in, out, begin, end, s);
-            default: return launch_tk<double, 2, 2, 16, 3, 2>(l, in, out, begin, end, s);
+            case 216: return launch_tk<double, 2, 2, 16, 3, 2>(l, in, out, begin, end, s);
+            case 20312: return launch_tk<double, 2, 3, 12, 3, 2, true>(l, in, out, begin, end, s);
+            default: return launch_tk<double, 2, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
             }
         }
         if (steps == 4) {
             switch (cfg) {
             case 408: return launch_tk<double, 2, 4, 8, 4, 2>(l, in, out, begin, end, s);
-            default: return launch_tk<double, 2, 2, 16, 4, 2>(l, in, out, begin, end, s);
+            case 216: return launch_tk<double, 2, 2, 16, 4, 2>(l, in, out, begin, end, s);
+            default: return launch_tk<double, 2, 2, 16, 4, 2, true>(l, in, out, begin, end, s);
             }
         }
     }
