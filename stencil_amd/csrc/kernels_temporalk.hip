@@ -85,7 +85,7 @@ struct TKTile {
 template <typename T, int V, int RY, int NW, int K, int R, bool DPPX>
 __global__ void __launch_bounds__(64 * NW)
     temporalk_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
-                  int zchunk, int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
+                  int zchunk, int tiles_x, int tiles_y, int halo_lo, int halo_hi, int remap, T avg) {
     using Tl = TKTile<T, V, RY, NW, K>;
     using VT = typename VecK<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
@@ -93,7 +93,14 @@ __global__ void __launch_bounds__(64 * NW)
     static_assert(R >= 2 && R % 2 == 0, "ring size must be even (z- parity) and >= 2");
     __shared__ __attribute__((aligned(16))) T L[K][LY][LX];
 
-    const int t = blockIdx.x;
+    // Optional XCD-aware order: workgroups are dealt round-robin to the 8
+    // XCDs, so give XCD j the j-th contiguous run of tiles (neighbours in x/y
+    // then share halo lines in that XCD's L2); uneven shares allowed.
+    int t = blockIdx.x;
+    if (remap) {
+        const int nb = gridDim.x, q = nb >> 3, r8 = nb & 7, j = t & 7;
+        t = j * q + (j < r8 ? j : r8) + (t >> 3);
+    }
     const int bx = t % tiles_x;
     const int by = (t / tiles_x) % tiles_y;
     const int bz = t / (tiles_x * tiles_y);
@@ -305,7 +312,7 @@ int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin,
                          (long long)l.zghost);
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, begin, end, zc, int(gx), int(gy),
-                       int(lo), int(hi), avg_weight<T>(l.prob));
+                       int(lo), int(hi), env_int("STENCIL_TK_REMAP", 0), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }

@@ -74,6 +74,12 @@ class JacobiEngine:
         # ghost/halo units per side of the slow axis (what a slab exchanges)
         self.depth = int(self.layout.zghost) if spec.dims == 3 else spec.radius
         self.fused = spec.fusable
+        # sweeps one fused launch performs (the library's own launch plan):
+        # 3 (or 4) for the 7-point star (TEMPORALK), 2 for the 27-point box
+        self.fuse_steps = 1
+        if self.fused:
+            launches, _ = self.plan(12)
+            self.fuse_steps = 12 // launches if launches and 12 % launches == 0 else 2
         self.slow_extent = int(self.lib.stencil_slow_extent(ctypes.byref(self.layout)))
         # one slow-axis unit = a whole plane (3D) or a whole padded row (2D)
         self.unit = int(self.layout.plane if spec.dims == 3 else self.layout.row)

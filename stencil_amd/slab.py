@@ -15,10 +15,11 @@ Per round, on each rank (overlap=True):
             neighbours (torch.distributed P2P; RCCL on GPUs, gloo on CPUs);
   stream B: update the interior planes meanwhile;
   join:     the next round waits for both streams and the received halos.
-A round is one sweep (halo depth r), or -- when the backend has the fused
-two-step kernel and 2-deep halos -- two sweeps in one launch per plane range
-(temporal blocking across GPUs: the exchange of 2 planes every 2 sweeps, the
-halo plane itself advanced to t+1 on chip by the fused kernel).
+A round is one sweep (halo depth r), or -- when the backend has a fused
+multi-step kernel and K-deep halos -- K sweeps in one launch per plane range
+(temporal blocking across GPUs: the exchange of K planes every K sweeps, the
+halo planes themselves advanced to t+K-1 .. t+1 on chip by the fused kernel;
+K = 3 for the 7-point star, 2 for the 27-point box).
 Every cell's arithmetic is the single-GPU kernel's, so results are bitwise
 identical for any number of ranks (tests/test_slab_gloo.py, tests/test_gpu_*).
 
@@ -102,6 +103,8 @@ class SlabJacobi:
         self.r = backend.r
         self.depth = backend.depth  # planes exchanged per side
         self.fused = bool(getattr(backend, "fused", False)) and self.depth >= 2
+        # sweeps per fused round: what the backend fuses, at most the halo depth
+        self.k = min(int(getattr(backend, "fuse_steps", 2)), self.depth) if self.fused else 1
         n = slab.count
         if slab.world > 1 and n < self.depth:
             raise ValueError(f"rank {slab.rank} owns {n} planes < halo depth {self.depth}; use fewer ranks")
@@ -189,6 +192,10 @@ class SlabJacobi:
         """Two sweeps, fused (needs backend.fused and halo depth >= 2)."""
         self._round(lambda s, d, b, e, st: self.be.sweep2(s, d, b, e, stream=st), self.depth)
 
+    def stepk(self, k: int) -> None:
+        """k sweeps fused in one launch per plane range (halo depth >= k)."""
+        self._round(lambda s, d, b, e, st: self.be.sweepk(s, d, b, e, k, stream=st), self.depth)
+
     def step2_split(self) -> None:
         """Two single sweeps per exchange of 2 planes (halo depth >= 2): the
         first sweep also advances the 1-deep halo planes of shared faces, the
@@ -255,7 +262,7 @@ class SlabJacobi:
 
     @property
     def mode(self) -> str:
-        """'fused' (two sweeps per launch), 'split2' (two single sweeps per
+        """'fused' (k sweeps per launch), 'split2' (two single sweeps per
         2-plane exchange) or 'single' (one sweep per 1-plane exchange)."""
         if self.fused:
             return "fused"
@@ -268,9 +275,14 @@ class SlabJacobi:
     def run(self, iterations: int) -> None:
         mode = self.mode
         if mode == "fused":
-            for _ in range(iterations // 2):
+            k = self.k
+            for _ in range(iterations // k):
+                self.stepk(k) if k != 2 else self.step2()
+            rem = iterations % k
+            if rem >= 2:
                 self.step2()
-            if iterations % 2:
+                rem -= 2
+            if rem:
                 self.step()
         elif mode == "split2":
             for _ in range(iterations // 2):
@@ -283,4 +295,4 @@ class SlabJacobi:
 
     def launches_per_round(self) -> int:
         """Sweeps per timed interior launch (the bench's roofline unit)."""
-        return 2 if self.fused else 1
+        return self.k if self.fused else 1

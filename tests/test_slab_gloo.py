@@ -26,8 +26,8 @@ class OracleSlabBackend:
     """Per-rank grid pair in the oracle's dense layout with `depth` halo
     planes per z side; sweeps run the oracle on plane ranges."""
 
-    def __init__(self, n, depth, lo_halo, hi_halo, fused):
-        self.r, self.depth, self.n = 1, depth, n
+    def __init__(self, n, depth, lo_halo, hi_halo, fused, fuse_steps=2):
+        self.r, self.depth, self.n, self.fuse_steps = 1, depth, n, fuse_steps
         self.lo_halo, self.hi_halo, self.fused = lo_halo, hi_halo, fused
         # the oracle's interior spans local planes -(depth-1) .. n+depth-2
         self.p = ob.problem(3, "fp64", "star", 1, "naive", NX, NY, n + 2 * (depth - 1))
@@ -57,13 +57,21 @@ class OracleSlabBackend:
         o = self.depth - 1
         ob.sweep(self.p, self._np(src), self._np(dst), b + o, e + o)
 
-    def sweep2(self, src, dst, b, e, stream=None):
+    def sweepk(self, src, dst, b, e, k, stream=None):
+        """k sweeps: intermediate step j (1..k-1) also advances the shared-face
+        halo planes k-j deep, as the fused kernels do."""
         o = self.depth - 1
-        lo = -1 if self.lo_halo else 0
-        hi = self.n + 1 if self.hi_halo else self.n
-        t1 = self._np(src).copy()  # ghost planes stay as in src (Dirichlet copy)
-        ob.sweep(self.p, self._np(src), t1, max(b - 1, lo) + o, min(e + 1, hi) + o)
-        ob.sweep(self.p, t1, self._np(dst), b + o, e + o)
+        cur = self._np(src)
+        for j in range(1, k):
+            lo = -(k - j) if self.lo_halo else 0
+            hi = self.n + (k - j) if self.hi_halo else self.n
+            t = cur.copy()  # ghost planes stay as in src (Dirichlet copy)
+            ob.sweep(self.p, cur, t, max(b - (k - j), lo) + o, min(e + (k - j), hi) + o)
+            cur = t
+        ob.sweep(self.p, cur, self._np(dst), b + o, e + o)
+
+    def sweep2(self, src, dst, b, e, stream=None):
+        self.sweepk(src, dst, b, e, 2)
 
 
 def _free_port():
@@ -74,12 +82,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, outdir, iterations, depth, fused, init, split2=True):
+def _worker(rank, world, port, outdir, iterations, depth, fused, init, split2=True, fuse_steps=2):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, count = partition(NZ, world, rank)
-    be = OracleSlabBackend(count, depth, rank > 0, rank < world - 1, fused)
+    be = OracleSlabBackend(count, depth, rank > 0, rank < world - 1, fused, fuse_steps)
     slab = SlabJacobi(be, SlabInfo(rank, world, first, count), TorchDistExchanger(rank, world))
     slab.split2 = split2
     slab.init(init, seed=31, plane_elems=NX * NY)
@@ -105,6 +113,21 @@ def test_slab_matches_single_process(world, depth, fused, split2, iterations):
                            nprocs=world, join=True, start_method="fork")
         got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)], axis=0)
     assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("depth,k", [(3, 3), (4, 3), (4, 4)])
+@pytest.mark.parametrize("iterations", [7, 8])
+def test_slab_k_step_rounds(world, depth, k, iterations):
+    """k fused sweeps per k-plane exchange (the TEMPORALK rounds), remainder
+    as a pair and/or a single sweep: bitwise equal to one process."""
+    p = ob.problem(3, "fp64", "star", 1, "naive", NX, NY, NZ)
+    want = ob.interior(p, ob.run(p, iterations, "random", 31))
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d, iterations, depth, True, "random", False, k),
+                           nprocs=world, join=True, start_method="fork")
+        got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)], axis=0)
     assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
 
 

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("temporal2_7pt", "zmarch7", "sweep_direct", "copy_kernel", "fill_initial_kernel", "plane_sums"):
+    for k in ("temporalk_7pt", "temporal2_7pt", "zmarch7", "sweep_direct", "copy_kernel", "fill_initial_kernel", "plane_sums"):
         if k in name:
             return k.replace("_7pt", "").replace("7", "") if k != "copy_kernel" else k
     return name[:40]
@@ -57,7 +57,7 @@ def main():
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     table = json.load(open(tpath)) if os.path.exists(tpath) else {}
     for k, ent in summary["kernels"].items():
-        if "hbm_bytes_per_launch" in ent and k in ("temporal2", "zmarch", "direct"):
+        if "hbm_bytes_per_launch" in ent and k in ("temporalk", "temporal2", "zmarch", "direct"):
             table.setdefault(workload, {})[k] = {"hbm_bytes_per_launch": round(ent["hbm_bytes_per_launch"]),
                                                  "source": f"profiles/{tag}_summary.json"}
     json.dump(table, open(tpath, "w"), indent=1)
