@@ -70,11 +70,15 @@ __device__ __forceinline__ double dpp_f(double v) {
 }
 constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
 
-template <typename T, int V, int RY, int NW, int K>
+template <typename T, int V, int RY, int NW, int K, bool AL = false, int XRO = 0>
 struct TKTile {
-    static constexpr int XR = (K + V - 1) / V;     // ring vectors per x side
+    static constexpr int XR = XRO ? XRO : (K + V - 1) / V;  // ring vectors per x side
     static constexpr int RW = 64 * V;              // region width
-    static constexpr int TX = RW - 2 * XR * V;     // output tile width
+    // output tile width; AL: a multiple of 128 B so every tile's output rows
+    // start on a cache line (the lanes past TX/V + 2 XR then idle)
+    static constexpr int AW = 128 / int(sizeof(T));
+    static constexpr int TX = AL ? (RW - 2 * XR * V) / AW * AW : RW - 2 * XR * V;
+    static constexpr int NL = TX / V + 2 * XR;     // lanes that load
     static constexpr int RH = NW * RY;             // region height
     static constexpr int TY = RH - 2 * K;          // output tile height
     static constexpr int LX = RW + 2 * V;          // LDS row: pad V | region | pad V
@@ -82,13 +86,13 @@ struct TKTile {
     static constexpr size_t lds_bytes = size_t(K) * LY * LX * sizeof(T);
 };
 
-template <typename T, int V, int RY, int NW, int K, int R, bool DPPX>
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX, bool AL, int XRO>
 __global__ void __launch_bounds__(64 * NW)
     temporalk_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
                   int zchunk, int tiles_x, int tiles_y, int halo_lo, int halo_hi, int remap, T avg) {
-    using Tl = TKTile<T, V, RY, NW, K>;
+    using Tl = TKTile<T, V, RY, NW, K, AL, XRO>;
     using VT = typename VecK<T, V>::type;
-    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
+    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY, NL = Tl::NL;
     static_assert(TY > 0 && TX > 0, "tile too small for K");
     static_assert(R >= 2 && R % 2 == 0, "ring size must be even (z- parity) and >= 2");
     __shared__ __attribute__((aligned(16))) T L[K][LY][LX];
@@ -129,9 +133,9 @@ __global__ void __launch_bounds__(64 * NW)
         const int rr = w + NW * k;
         const int64_t y = y0 + rr;
         off[k] = y * g.row + x;
-        ldok[k] = y >= -1 && y <= g.ny && x <= g.nx;
+        ldok[k] = y >= -1 && y <= g.ny && x <= g.nx && lane < NL;
         yin[k] = y >= 0 && y < g.ny;
-        st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < 64 - XR;
+        st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < NL - XR;
     }
     bool xin[V], xst[V];
 #pragma unroll
@@ -267,15 +271,15 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false>
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false, bool AL = false, int XRO = 0>
 int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
-    using Tl = TKTile<T, V, RY, NW, K>;
+    using Tl = TKTile<T, V, RY, NW, K, AL, XRO>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = temporalk_7pt<T, V, RY, NW, K, R, DPPX>;
+    auto kern = temporalk_7pt<T, V, RY, NW, K, R, DPPX, AL, XRO>;
     int zc = env_int("STENCIL_TK_ZCHUNK", 0);
     if (zc <= 0) {
         // Chunk count c minimising  ceil(tiles*c / slots) * (nz/c + 2K):
@@ -334,6 +338,7 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
             case 608: return launch_tk<float, 4, 6, 8, 3, 2>(l, in, out, begin, end, s);
             case 216: return launch_tk<float, 4, 2, 16, 3, 2>(l, in, out, begin, end, s);
             case 30216: return launch_tk<float, 2, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
+            case 40216: return launch_tk<float, 4, 2, 16, 3, 2, true, true>(l, in, out, begin, end, s);
             case 30316: return launch_tk<float, 2, 3, 16, 3, 2, true>(l, in, out, begin, end, s);
             default: return launch_tk<float, 4, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
             }
@@ -352,12 +357,16 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
             case 10216: return launch_tk<double, 2, 2, 16, 3, 4>(l, in, out, begin, end, s);
             case 216: return launch_tk<double, 2, 2, 16, 3, 2>(l, in, out, begin, end, s);
             case 20312: return launch_tk<double, 2, 3, 12, 3, 2, true>(l, in, out, begin, end, s);
+            case 20412: return launch_tk<double, 2, 4, 12, 3, 2, true>(l, in, out, begin, end, s);
+            case 20408: return launch_tk<double, 2, 4, 8, 3, 2, true>(l, in, out, begin, end, s);
+            case 40216: return launch_tk<double, 2, 2, 16, 3, 2, true, true>(l, in, out, begin, end, s);
             default: return launch_tk<double, 2, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
             }
         }
         if (steps == 4) {
             switch (cfg) {
             case 408: return launch_tk<double, 2, 4, 8, 4, 2>(l, in, out, begin, end, s);
+            case 20408: return launch_tk<double, 2, 4, 8, 4, 2, true>(l, in, out, begin, end, s);
             case 216: return launch_tk<double, 2, 2, 16, 4, 2>(l, in, out, begin, end, s);
             default: return launch_tk<double, 2, 2, 16, 4, 2, true>(l, in, out, begin, end, s);
             }

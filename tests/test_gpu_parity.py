@@ -129,7 +129,7 @@ def test_temporal2_chunking(gpu, monkeypatch, zchunk, dtype, stencil, t2cfg):
         assert same_bits(got, want), it
 
 
-@pytest.mark.parametrize("steps,cfg", [("3", "default"), ("3", "312"), ("3", "608"), ("3", "216"), ("3", "20312"), ("3", "30216"), ("4", "default"),
+@pytest.mark.parametrize("steps,cfg", [("3", "default"), ("3", "312"), ("3", "608"), ("3", "216"), ("3", "20312"), ("3", "30216"), ("3", "40216"), ("4", "default"),
                                        ("4", "408")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])

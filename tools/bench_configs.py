@@ -42,7 +42,7 @@ def run(name, c):
     launches, kernel = e.plan(iters)
     cells = nx * ny * nz
     out = {"config": name, "grid": [nx, ny, nz], "dims": spec.dims, "dtype": spec.dtype, "shape": spec.shape,
-           "order": spec.order, "iterations": iters, "kernel": {1: "direct", 2: "zmarch", 3: "temporal2"}[kernel],
+           "order": spec.order, "iterations": iters, "kernel": {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel],
            "launches": launches, "device_ms": round(dev_ms, 4), "wall_ms": round(wall * 1e3, 4),
            "gcell_per_s": round(cells * iters / (dev_ms * 1e-3) / 1e9, 2),
            "alg_GBps": round(cells * iters * 2 * spec.elem_bytes / (dev_ms * 1e-3) / 1e9, 1)}
