@@ -56,16 +56,18 @@ __device__ __forceinline__ float fma0(float s, float a) { return __builtin_fmaf(
 __device__ __forceinline__ double fma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
 
 // Whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1): lane i receives
-// lane i-1's (shr) or lane i+1's (shl) value; the lane without a source gets 0.
+// lane i-1's (shr) or lane i+1's (shl) value; the lane without a source gets
+// 0 (bound_ctrl: no "old" operand to initialise -- that lane is a ring lane
+// whose value is never used).
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_f(double v) {
     const int2 b = __builtin_bit_cast(int2, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, b.x, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, b.y, CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(b.x, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(b.y, CTRL, 0xf, 0xf, true);
     return __builtin_bit_cast(double, make_int2(lo, hi));
 }
 constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
@@ -86,8 +88,8 @@ struct TKTile {
     static constexpr size_t lds_bytes = size_t(K) * LY * LX * sizeof(T);
 };
 
-template <typename T, int V, int RY, int NW, int K, int R, bool DPPX, bool AL, int XRO>
-__global__ void __launch_bounds__(64 * NW)
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX, bool AL, int XRO, int WPE, bool SB = false>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE)))
     temporalk_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend,
                   int zchunk, int tiles_x, int tiles_y, int halo_lo, int halo_hi, int remap, T avg) {
     using Tl = TKTile<T, V, RY, NW, K, AL, XRO>;
@@ -126,14 +128,23 @@ __global__ void __launch_bounds__(64 * NW)
         for (int i = threadIdx.y * 64 + threadIdx.x; i < N16; i += 64 * NW) l16[i] = VT{};
     }
 
-    int64_t off[RY];
-    bool ldok[RY], yin[RY], st[RY];
+    // Loads are issued unconditionally from clamped addresses (rows outside
+    // [-1, ny], vectors past x = nx, idle lanes, planes outside the loaded
+    // range re-read valid cells that only feed ring cells): with no branch
+    // around them the compiler can wait for plane p with vmcnt(RY) instead of
+    // vmcnt(0) -- a conditional load or store leaves a path with no younger
+    // memory op, and vmcnt(0) also waits for the prefetched plane p+1.
+    int off[RY];  // in-plane offsets (a plane has < 2^31 elements, checked at launch)
+    bool yin[RY], st[RY];
+    const int64_t xmax = g.nx / V * V;  // last vector start that stays inside the padded row
+    const int64_t xl = lane < NL ? x : int64_t(bx) * TX - XR * V + int64_t(NL - 1) * V;
+    const int64_t xc = xl < xmax ? xl : xmax;
 #pragma unroll
     for (int k = 0; k < RY; ++k) {
         const int rr = w + NW * k;
         const int64_t y = y0 + rr;
-        off[k] = y * g.row + x;
-        ldok[k] = y >= -1 && y <= g.ny && x <= g.nx && lane < NL;
+        const int64_t yc = y < -1 ? -1 : (y > g.ny ? g.ny : y);
+        off[k] = int(yc * g.row + xc);
         yin[k] = y >= 0 && y < g.ny;
         st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < NL - XR;
     }
@@ -150,11 +161,10 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
 
     auto load_plane = [&](VT (&d)[RY], int64_t z) {
-        if (z >= ld_lo && z <= zlast) {
+        const int64_t zc = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
+        const T* base = src + zc * plane;
 #pragma unroll
-            for (int k = 0; k < RY; ++k)
-                if (ldok[k]) d[k] = *reinterpret_cast<const VT*>(src + z * plane + off[k]);
-        }
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + int64_t(off[k]));
     };
 
     const int64_t p0 = za - K;
@@ -217,6 +227,7 @@ __global__ void __launch_bounds__(64 * NW)
                 hz[P][s - 1][k] = c;
                 res[s - 1][k] = o;
             }
+            if constexpr (SB) __builtin_amdgcn_sched_barrier(0);  // no hoisting across stages
         }
         // t_K(p-K) -> HBM
         const int64_t zo = p - K;
@@ -224,7 +235,7 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
                 if (st[k]) {
-                    T* q = dst + zo * plane + off[k];
+                    T* q = dst + zo * plane + int64_t(off[k]);
                     if (xst[V - 1]) {
                         __builtin_nontemporal_store(res[K - 1][k], reinterpret_cast<VT*>(q));
                     } else {
@@ -271,7 +282,8 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false, bool AL = false, int XRO = 0>
+template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false, bool AL = false, int XRO = 0,
+          int WPE = 1, bool SB = false>
 int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
     using Tl = TKTile<T, V, RY, NW, K, AL, XRO>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
@@ -279,7 +291,8 @@ int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = temporalk_7pt<T, V, RY, NW, K, R, DPPX, AL, XRO>;
+    auto kern = temporalk_7pt<T, V, RY, NW, K, R, DPPX, AL, XRO, WPE, SB>;
+    if (g.plane >= (int64_t(1) << 31)) return set_error(STENCIL_EINVAL, "plane too large for temporalk (2^31 elements)");
     int zc = env_int("STENCIL_TK_ZCHUNK", 0);
     if (zc <= 0) {
         // Chunk count c minimising  ceil(tiles*c / slots) * (nz/c + 2K):
@@ -354,11 +367,11 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
         if (steps == 3) {
             switch (cfg) {
             case 312: return launch_tk<double, 2, 3, 12, 3, 2>(l, in, out, begin, end, s);
-            case 10216: return launch_tk<double, 2, 2, 16, 3, 4>(l, in, out, begin, end, s);
             case 216: return launch_tk<double, 2, 2, 16, 3, 2>(l, in, out, begin, end, s);
             case 20312: return launch_tk<double, 2, 3, 12, 3, 2, true>(l, in, out, begin, end, s);
             case 20412: return launch_tk<double, 2, 4, 12, 3, 2, true>(l, in, out, begin, end, s);
             case 20408: return launch_tk<double, 2, 4, 8, 3, 2, true>(l, in, out, begin, end, s);
+            case 20216 + 40000: return launch_tk<double, 2, 2, 16, 3, 4, true>(l, in, out, begin, end, s);
             case 40216: return launch_tk<double, 2, 2, 16, 3, 2, true, true>(l, in, out, begin, end, s);
             default: return launch_tk<double, 2, 2, 16, 3, 2, true>(l, in, out, begin, end, s);
             }
