@@ -178,7 +178,9 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
                    void* stream);
 
 /* K fused sweeps, out = S^K(in) on [begin, end): steps 1 = stencil_sweep,
- * 2 = stencil_sweep2, 3 or 4 = the TEMPORALK kernel (3D 7-point star only).
+ * 2 = stencil_sweep2, 3 or 4 = the TEMPORALK kernel (3D 7-point star), 3 =
+ * the K-step box kernel (3D 27-point box; kernels_boxk.hip, which also serves
+ * the box's 2-step sweep2).
  * With HALO_LO/HI flags the grid needs halo >= steps. */
 int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
                    int32_t steps, void* stream);

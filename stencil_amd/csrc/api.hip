@@ -120,8 +120,13 @@ int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b,
     return launch_direct(l, in, out, b, e, s);
 }
 
+// Two fused sweeps.  27-point box: the two-phase K-step kernel
+// (kernels_boxk.hip); STENCIL_BOXK=0 selects the earlier box27_zmarch<2>.
 int launch_fused(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
-    return temporal2_supports(l.prob) ? launch_temporal2(l, in, out, b, e, s) : launch_box27(l, in, out, b, e, 2, s);
+    if (temporal2_supports(l.prob)) return launch_temporal2(l, in, out, b, e, s);
+    const char* k = std::getenv("STENCIL_BOXK");
+    if (k && *k == '0') return launch_box27(l, in, out, b, e, 2, s);
+    return launch_boxk(l, in, out, b, e, 2, s);
 }
 
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
@@ -394,12 +399,15 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
     if (steps == 2) return stencil_sweep2(l, in, out, begin, end, stream);
     if (int rc = check_layout(l)) return rc;
     if (steps != 3 && steps != 4) return set_error(STENCIL_EINVAL, "steps must be 1..4 (got %d)", steps);
-    if (!temporal2_supports(l->prob))
-        return set_error(STENCIL_EUNSUPPORTED, "3- and 4-step fused sweeps cover the 3D r=1 naive 7-point star only");
+    const bool box = box27_supports(l->prob);
+    if (!temporal2_supports(l->prob) && !(box && steps == 3))
+        return set_error(STENCIL_EUNSUPPORTED,
+                         "3- and 4-step fused sweeps cover the 3D r=1 naive 7-point star (3, 4) and box (3) only");
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
-    const int rc = launch_temporalk(*l, in, out, begin, end, steps, as_stream(stream));
+    const int rc = box ? launch_boxk(*l, in, out, begin, end, steps, as_stream(stream))
+                       : launch_temporalk(*l, in, out, begin, end, steps, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();
     return rc;
 }

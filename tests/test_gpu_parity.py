@@ -151,15 +151,46 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
     assert e.plan(9) == (9 // k + (9 % k) // 2 + (9 % k) % 2, 4)
 
 
-@pytest.mark.parametrize("steps", [3, 4])
+@pytest.mark.parametrize("cfg", ["default", "308", "216"])
+@pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-def test_temporalk_signed_zero_field(gpu, steps, dtype):
+def test_boxk_chunking(gpu, monkeypatch, cfg, zchunk, dtype):
+    """27-point box, two fused sweeps per launch through the K-step box kernel
+    (kernels_boxk.hip): workgroup shapes (incl. spilling ones), forced z-chunks
+    shorter and longer than the 3K-plane pipeline fill, odd iteration counts."""
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_BOXK_CFG", cfg)
+    nx, ny, nz = 131, 61, 29
+    p = ob.problem(3, dtype, "box", 1, "naive", nx, ny, nz)
+    for it in (2, 3, 4, 5):
+        want = ob.run(p, it, "random", 21 + it)
+        _, got = gpu_run(gpu, 3, dtype, "box", 1, "naive", "temporal2", nx, ny, nz, it, "random", 21 + it)
+        assert same_bits(got, want), it
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("shape3", [(131, 61, 29), (7, 5, 3), (250, 19, 12)])
+def test_boxk_three_steps(gpu, dtype, shape3):
+    """stencil_sweepk(3) on the 27-point box equals three plain sweeps."""
+    nx, ny, nz = shape3
+    p = ob.problem(3, dtype, "box", 1, "naive", nx, ny, nz)
+    want = ob.run(p, 3, "random", 5)
+    e = engine(gpu, 3, dtype, "box", 1, "naive", "auto", nx, ny, nz)
+    e.reset("random", 5)
+    e.sweepk(e.a, e.b, 0, nz, 3)
+    assert same_bits(e.to_numpy(e.b), want)
+
+
+@pytest.mark.parametrize("shape,steps", [("star", 3), ("star", 4), ("box", 2), ("box", 3)])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_temporalk_signed_zero_field(gpu, shape, steps, dtype):
     """The K-step kernel folds the reference's leading `0 +` into
     fma(sum, avg, +0); a block of -0.0 cells (where 0 + -0 = +0 matters) and
     mixed-sign data must still match plain sweeps bit for bit."""
     import torch
     nx, ny, nz = 77, 40, 23
-    e = engine(gpu, 3, dtype, "star", 1, "naive", "temporalk", nx, ny, nz)
+    e = engine(gpu, 3, dtype, shape, 1, "naive", "temporalk" if shape == "star" else "temporal2", nx, ny, nz)
     e.reset("random", 11)
     full = e.with_ghosts(e.a)
     inner = e.interior(e.a)
@@ -167,7 +198,7 @@ def test_temporalk_signed_zero_field(gpu, steps, dtype):
     inner[15:20] *= -1.0
     torch.cuda.synchronize()
     start = full.cpu().numpy().copy()
-    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    p = ob.problem(3, dtype, shape, 1, "naive", nx, ny, nz)
     a, b = start.copy(), start.copy()
     for _ in range(steps):
         ob.sweep(p, a, b, 0, nz)

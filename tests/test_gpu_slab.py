@@ -81,21 +81,23 @@ def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split, shape):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("shape,k", [("star", 3), ("star", 4), ("box", 2), ("box", 3)])
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("cfg", ["default", "312"])
-def test_slabs_k_step_rounds(gpu, monkeypatch, world, k, split, cfg):
-    """k fused sweeps per k-plane halo exchange (TEMPORALK with HALO_LO/HI):
-    halo planes advanced to t+k-1 .. t+1 inside the launch."""
+def test_slabs_k_step_rounds(gpu, monkeypatch, world, shape, k, split, cfg):
+    """k fused sweeps per k-plane halo exchange (TEMPORALK / the K-step box
+    kernel with HALO_LO/HI): halo planes advanced to t+k-1 .. t+1 inside the
+    launch."""
     if cfg != "default":
         monkeypatch.setenv("STENCIL_TK_CFG", cfg)
     monkeypatch.setenv("STENCIL_TK_ZCHUNK", "5")
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", "5")
     nx, ny, nz, it = 70, 45, 29, 11
-    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", kernel="direct"), nx, ny, nz, device=gpu)
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", kernel="direct", shape=shape), nx, ny, nz, device=gpu)
     ref.reset("random", 17)
     fin, _ = ref.iterate(it)
-    got = run_slabs(gpu, nx, ny, nz, world, it, True, split, k=k)
+    got = run_slabs(gpu, nx, ny, nz, world, it, True, split, shape=shape, k=k)
     assert torch.equal(got, ref.interior(fin))
 
 
