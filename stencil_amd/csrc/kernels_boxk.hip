@@ -210,6 +210,9 @@ __global__ void __launch_bounds__(64 * NW)
                 cen[P][s - 1][k] = cc;
                 res[s - 1][k] = o;
             }
+#ifdef BOXK_SB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
         // t_K(p-2K) -> HBM
         const int64_t zo = p - 2 * K;
@@ -319,10 +322,17 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         if (steps == 2) {
             switch (cfg) {
             case 408: return launch_bk<float, 4, 4, 8, 2, 2>(l, in, out, begin, end, s);
-            default: return launch_bk<float, 4, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            case 208: return launch_bk<float, 4, 2, 8, 2, 2>(l, in, out, begin, end, s);
+            case 116: return launch_bk<float, 4, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            default: return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
             }
         }
-        if (steps == 3) return launch_bk<float, 4, 4, 8, 3, 2>(l, in, out, begin, end, s);
+        if (steps == 3) {
+            switch (cfg) {
+            case 208: return launch_bk<float, 4, 2, 8, 3, 2>(l, in, out, begin, end, s);
+            default: return launch_bk<float, 4, 1, 16, 3, 2>(l, in, out, begin, end, s);
+            }
+        }
     } else {
         if (steps == 2) {
             switch (cfg) {
@@ -330,10 +340,18 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 308: return launch_bk<double, 2, 3, 8, 2, 2>(l, in, out, begin, end, s);
             case 408: return launch_bk<double, 2, 4, 8, 2, 2>(l, in, out, begin, end, s);
             case 212: return launch_bk<double, 2, 2, 12, 2, 2>(l, in, out, begin, end, s);
+            case 208: return launch_bk<double, 2, 2, 8, 2, 2>(l, in, out, begin, end, s);
             default: return launch_bk<double, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
             }
         }
-        if (steps == 3) return launch_bk<double, 2, 4, 8, 3, 2>(l, in, out, begin, end, s);
+        if (steps == 3) {
+            switch (cfg) {
+            case 208: return launch_bk<double, 2, 2, 8, 3, 2>(l, in, out, begin, end, s);
+            case 308: return launch_bk<double, 2, 3, 8, 3, 2>(l, in, out, begin, end, s);
+            case 408: return launch_bk<double, 2, 4, 8, 3, 2>(l, in, out, begin, end, s);
+            default: return launch_bk<double, 2, 1, 16, 3, 2>(l, in, out, begin, end, s);
+            }
+        }
     }
     return set_error(STENCIL_EINVAL, "boxk steps must be 2 or 3 (got %d)", steps);
 }

@@ -45,8 +45,8 @@ class StencilSpec:
         """Does the fused two-step kernel cover this stencil?"""
         if self.dims != 3 or self.radius != 1 or self.order != "naive":
             return False
-        # the fused 27-point kernel is slower than its single sweep (DESIGN.md §5): explicit only
-        return self.kernel in ("temporal2", "temporalk") or (self.kernel == "auto" and self.shape == "star")
+        # AUTO fuses both: TEMPORALK for the 7-point star, the 2-step BOXK kernel for the box
+        return self.kernel in ("temporal2", "temporalk", "auto")
 
     @property
     def elem_bytes(self) -> int:

@@ -1,6 +1,8 @@
 """Interleaved A/B timing of kernel variants selected by environment knobs
 (one process, several rounds; see cdna_hip_programming.md §5.4 rule 24).
-usage: python tools/tune.py [n] [variants-json]"""
+usage: python tools/tune.py [n] [variants-json]
+TUNE_SWEEPK=k times k-step stencil_sweepk launches over the whole grid instead
+of stencil_iterate (the only way to reach e.g. the 3-step box kernel)."""
 import json
 import os
 import sys
@@ -11,6 +13,23 @@ import torch  # noqa: E402
 from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth  # noqa: E402
 
 
+def time_sweepk(eng, k, iters):
+    """ms for `iters` sweeps done as iters//k k-step launches (a <-> b)."""
+    n = eng.slow_extent
+    launches = max(1, iters // k)
+    for _ in range(2):
+        eng.sweepk(eng.a, eng.b, 0, n, k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    src, dst = eng.a, eng.b
+    for _ in range(launches):
+        eng.sweepk(src, dst, 0, n, k)
+        src, dst = dst, src
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * iters / (launches * k)
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     variants = json.loads(sys.argv[2]) if len(sys.argv) > 2 else [{}]
@@ -19,6 +38,7 @@ def main():
     iters = int(os.environ.get("TUNE_ITERS", "50"))
     shape = [int(v) for v in os.environ.get("TUNE_SHAPE", f"{n},{n},{n}").split(",")]
     stencil = os.environ.get("TUNE_STENCIL", "star")
+    sweepk = int(os.environ.get("TUNE_SWEEPK", "0"))
     eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel, shape=stencil), *shape)
     cells = shape[0] * shape[1] * shape[2]
     eng.reset()
@@ -33,9 +53,11 @@ def main():
                     del os.environ[k]
             os.environ.update(base_env)
             os.environ.update({k: str(x) for k, x in v.items()})
-            eng.iterate(4)
-            _, ms = eng.iterate(iters, timed=True)
-            launches = eng.plan(iters)[0]
+            if sweepk:
+                ms = time_sweepk(eng, sweepk, iters)
+            else:
+                eng.iterate(4)
+                _, ms = eng.iterate(iters, timed=True)
             res[i].append(ms / iters)
     for i, v in enumerate(variants):
         t = sorted(res[i])
