@@ -7,9 +7,10 @@
 One step = one Jacobi sweep of the whole grid.  At N=1 the workload is
 BASELINE config 2 (512^3 interior, fp64, 7-point star; the default K=1000 is
 exactly its 1000 iterations).  At N>1 every rank owns a 512^3 Z-slab of a
-512 x 512 x 512N grid (weak scaling) and exchanges one halo plane with each
-neighbour per sweep over RCCL, overlapped with the interior sweep -- or, with
-the fused two-step kernel, two planes per pair of sweeps.
+512 x 512 x 512N grid (weak scaling) and exchanges K halo planes with each
+neighbour per round of K fused sweeps (K = 4: the strip-layout K-step
+kernel) over RCCL, the boundary planes' launch and the send/recv overlapped
+with the interior launch on a second stream.
 
 Rank 0 prints one JSON line with the whole-job rate, the live roofline of the
 dominant kernel (algorithmic bytes per launch / average launch time from HIP
@@ -101,7 +102,7 @@ def main():
 
     n = args.n
     # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
-    # 3 for the 7-point star) so K sweeps fuse across the exchange too (one
+    # 4 for the 7-point star) so K sweeps fuse across the exchange too (one
     # K-plane exchange per K-sweep round).
     spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=1, order="naive", kernel=args.kernel)
     fuse = JacobiEngine(spec, n, n, n, device=local, allocate=False).fuse_steps
@@ -156,8 +157,9 @@ def main():
     cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (n - 2 * edge) / n
     alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
     if world == 1:
-        # device time per `sweeps_per_launch` sweeps: with K = 3 a 1000-step
-        # job is 333 fused launches + 1 single sweep, charged pro rata
+        # device time per `sweeps_per_launch` sweeps, charged pro rata (with
+        # K = 4 a 1000-step job is 250 fused launches; a K that does not divide
+        # the step count adds a remainder pair / single sweep)
         launch_ms = kernel_ms_total * sweeps_per_launch / max(1, args.steps)
     else:
         launch_ms = kernel_ms_total / max(1, kernel_launches)

@@ -97,7 +97,7 @@ enum {
     STENCIL_KERNEL_ZMARCH = 2,    /* 2.5D: LDS plane + z register queue */
     STENCIL_KERNEL_TEMPORAL2 = 3, /* ZMARCH with 2 fused time steps per launch */
     STENCIL_KERNEL_TEMPORALK = 4  /* 3D 7-point star: K = 3 or 4 fused steps per launch
-                                     (K = env STENCIL_TK_STEPS, default 3) */
+                                     (K = env STENCIL_TK_STEPS, default 4) */
 };
 enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
 /* stencil_problem.flags: which z faces of this grid are halos filled by a

@@ -80,7 +80,7 @@ int sweep_family(const stencil_problem& p) {
 // a problem a fused kernel supports (STENCIL_NO_T2=1 disables the latter).
 bool iterate_fused(const stencil_problem& p) {
     if (p.kernel == STENCIL_KERNEL_TEMPORAL2 || p.kernel == STENCIL_KERNEL_TEMPORALK) return true;
-    // AUTO fuses the 7-point star (TEMPORALK, K = 3) and the 27-point box
+    // AUTO fuses the 7-point star (TEMPORALK, K = 4) and the 27-point box
     // (the 2-step BOXK kernel: +50-90 % fp64, +9-37 % fp32 over the single
     // sweep on MI355X).
     if (p.kernel != STENCIL_KERNEL_AUTO || !fused_supported(p)) return false;
@@ -88,8 +88,9 @@ bool iterate_fused(const stencil_problem& p) {
     return !(e && *e && *e != '0');
 }
 
-// Steps per launch of the deep temporal-blocking family (kernels_temporalk.hip)
-// in stencil_iterate: K = STENCIL_TK_STEPS (3 or 4, default 3) for explicit
+// Steps per launch of the deep temporal-blocking family (kernels_strip.hip,
+// kernels_temporalk.hip) in stencil_iterate: K = STENCIL_TK_STEPS (3 or 4,
+// default 4) for explicit
 // TEMPORALK and for AUTO on the 7-point star (STENCIL_NO_TK=1 or
 // STENCIL_NO_T2=1 turn the latter off); 0 = not used.
 int iterate_tk_steps(const stencil_problem& p) {
@@ -102,7 +103,7 @@ int iterate_tk_steps(const stencil_problem& p) {
         return 0;
     }
     const char* k = std::getenv("STENCIL_TK_STEPS");
-    const int steps = k && *k ? std::atoi(k) : 3;
+    const int steps = k && *k ? std::atoi(k) : 4;
     return steps == 3 || steps == 4 ? steps : 0;
 }
 

@@ -68,6 +68,8 @@ int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t
                      int64_t end, hipStream_t s);
 int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
                      int steps, hipStream_t s);
+int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                   int cfg, hipStream_t s);
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                 hipStream_t s);
 bool zmarch_supports(const stencil_problem& p);

@@ -1,0 +1,389 @@
+// kernels_strip.hip -- K fused Jacobi sweeps per launch for the 3D 7-point
+// star (r = 1, naive order) with every wave owning a STRIP of consecutive
+// rows: the "strip" layout of the K-step z-march of kernels_temporalk.hip.
+//
+// Why.  In kernels_temporalk.hip a wave owns rows w, w+NW, ... of the
+// region, so every y-neighbour and every centre comes from LDS: per plane
+// and wave 3*RY reads and RY writes of 1 KiB per stage, two barriers per
+// plane.  On MI355X a ds_write_b128 costs ~13 LDS cycles and a ds_read_b128
+// 4, which at 16 waves/CU is ~2400 LDS cycles per plane step -- as long as
+// the VALU work, and the kernel does not speed up when its HBM bytes drop
+// (DESIGN.md §5).  Here wave w owns region rows [w*RY, w*RY + RY):
+//   * centre, y-neighbours inside the strip and z-neighbours come from the
+//     lane's own registers, x-neighbours from DPP lane shifts;
+//   * only the strip's first and last rows go through LDS (the row above /
+//     below the strip is the neighbour wave's last / first row): 2 writes
+//     and 2 reads per stage and wave;
+//   * the boundary-row buffers are double-buffered by plane parity, so one
+//     barrier per plane suffices (a wave that passed barrier p has every
+//     wave's reads of plane p-1's buffer behind it).
+//
+// Pipeline (as kernels_temporalk.hip): at plane step p stage s computes
+// t_s(p-s) from t_{s-1}(p-s-1) (z-), t_{s-1}(p-s) (centre + x/y) and
+// t_{s-1}(p-s+1) (z+, stage s-1's result of this step; stage 1: in(p)).
+// Per lane and stage the two older planes live in a 2-slot register history
+// H (slot = plane parity), the input in a 4-slot ring (in(p-2) .. in(p+1),
+// loads issued two planes ahead).  t_K(p-K) goes to HBM (nontemporal).
+//
+// Per step:
+//   barrier
+//   read phase   boundary rows of t_{s-1}(p-s) from buffer (p-1)&1,
+//                stages 1..K, store t_K(p-K)
+//   write phase  boundary rows of in(p), t_1(p-1) .. t_{K-1}(p-K+1) into
+//                buffer p&1; request in(p+2)
+//
+// Arithmetic is the single sweep's (0 + x- + x+ + y- + y+ + z- + z+) * avg
+// with the "0 +" folded into fma(sum, avg, +0) exactly as in
+// kernels_temporalk.hip; intermediate planes keep ghost cells at their input
+// value; slab-halo planes (HALO_LO/HI) are advanced.  Bitwise equal to K
+// plain sweeps (tests/test_gpu_parity.py).
+#include <cstdlib>
+
+#include "common.hpp"
+
+namespace stencil {
+namespace {
+
+template <typename T, int V>
+struct VecS {
+    typedef T type __attribute__((ext_vector_type(V)));
+};
+
+__device__ __forceinline__ float sfma0(float s, float a) { return __builtin_fmaf(s, a, 0.0f); }
+__device__ __forceinline__ double sfma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
+
+template <int CTRL>
+__device__ __forceinline__ float sdpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double sdpp(double v) {
+    const int2 b = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_mov_dpp(b.x, CTRL, 0xf, 0xf, true),
+                                                 __builtin_amdgcn_mov_dpp(b.y, CTRL, 0xf, 0xf, true)));
+}
+constexpr int kSShr1 = 0x138, kSShl1 = 0x130;  // wave_shr:1 / wave_shl:1
+
+template <typename T, int V, int RY, int NW, int K, bool DB>
+struct StripTile {
+    static constexpr int XR = (K + V - 1) / V;  // ring vectors per x side
+    static constexpr int RW = 64 * V;           // region width
+    static constexpr int TX = RW - 2 * XR * V;  // output tile width
+    static constexpr int RH = NW * RY;          // region height
+    static constexpr int TY = RH - 2 * K;       // output tile height
+    static constexpr int NB = DB ? 2 : 1;       // boundary-row buffers (plane parity)
+    // boundary rows: [buffer][stage input][wave][top, bottom][RW]
+    static constexpr size_t lds_bytes = size_t(NB) * K * NW * 2 * RW * sizeof(T);
+};
+
+// DIAG (timing experiments only, results are wrong): 1 = no loads after the
+// first two planes, 2 = no arithmetic (t_s = centre), 3 = no stores
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0>
+__global__ void __launch_bounds__(64 * NW)
+    tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend, int zchunk,
+                int tiles_x, int tiles_y, int halo_lo, int halo_hi, int remap, T avg) {
+    using Tl = StripTile<T, V, RY, NW, K, DB>;
+    using VT = typename VecS<T, V>::type;
+    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
+    static_assert(TY > 0 && TX > 0, "tile too small for K");
+    static_assert(RY >= 2, "a strip needs a first and a last row");
+    __shared__ __attribute__((aligned(16))) T L[NB][K][NW][2][RW];
+
+    int t = blockIdx.x;
+    if (remap) {  // XCD j gets the j-th contiguous run of tiles (see kernels_temporalk.hip)
+        const int nb = gridDim.x, q = nb >> 3, r8 = nb & 7, j = t & 7;
+        t = j * q + (j < r8 ? j : r8) + (t >> 3);
+    }
+    const int bx = t % tiles_x;
+    const int by = (t / tiles_x) % tiles_y;
+    const int bz = t / (tiles_x * tiles_y);
+
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
+    const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
+    // z bookkeeping in 32 bits (nz < 2^31, checked at launch) so it stays scalar
+    const int za = int(zbeg) + bz * zchunk;
+    const int zb = za + zchunk < int(zend) ? za + zchunk : int(zend);
+    const int nz = int(g.nz);
+    const int64_t plane = g.plane;
+    // Addresses are a uniform per-plane base (SGPRs) + a non-negative 32-bit
+    // byte offset per row (one VGPR, shared by loads and stores): the
+    // saddr form of global_load/store.  bias moves the lowest offset (row -1,
+    // x = -XR*V) to >= 0.
+    const int64_t bias = g.row + XR * V;
+    const char* __restrict__ src = reinterpret_cast<const char*>(in + g.origin - bias);
+    char* __restrict__ dst = reinterpret_cast<char*>(out + g.origin - bias);
+
+    {
+        constexpr int N16 = int(Tl::lds_bytes / 16);
+        VT* l16 = reinterpret_cast<VT*>(&L[0][0][0][0][0]);
+        for (int i = threadIdx.y * 64 + threadIdx.x; i < N16; i += 64 * NW) l16[i] = VT{};
+    }
+
+    // Unconditional loads from clamped addresses (kernels_temporalk.hip): the
+    // plane wait is then a counted vmcnt, not vmcnt(0).
+    uint32_t off[RY];  // byte offset of this lane's vector in row k, from the biased plane base
+    bool yin[RY], st[RY];
+    const int64_t xmax = g.nx / V * V;
+    const int64_t xc = x < xmax ? x : xmax;
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int rr = w * RY + k;
+        const int64_t y = y0 + k;
+        const int64_t yc = y < -1 ? -1 : (y > g.ny ? g.ny : y);
+        off[k] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
+        yin[k] = y >= 0 && y < g.ny;
+        st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < 64 - XR;
+    }
+    bool xin[V], xst[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        xin[j] = x + j >= 0 && x + j < g.nx;
+        xst[j] = x + j < g.nx;
+    }
+    const int ld_lo = halo_lo ? -K : -1;
+    const int ld_hi = halo_hi ? nz + K - 1 : nz;
+    const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
+    auto load_plane = [&](VT (&d)[RY], int z) {
+        const int zz = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
+        const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
+#pragma unroll
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
+    };
+
+    const int p0 = za - K;
+    VT vin[4][RY];                  // slot (q - p0) & 3 holds in(q)
+    VT H[K > 1 ? K - 1 : 1][2][RY]; // H[s-1][(q - p0) & 1] holds t_s(q), s < K
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < RY; ++k) vin[i][k] = VT{};
+#pragma unroll
+    for (int s = 0; s < (K > 1 ? K - 1 : 1); ++s)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int k = 0; k < RY; ++k) H[s][b][k] = VT{};
+    load_plane(vin[0], p0);
+    load_plane(vin[1], p0 + 1);
+
+    const int xl = lane * V;
+    // neighbour strips (the first / last wave reads its own: those rows are ring rows)
+    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+
+    auto step = [&](auto S_, int p) {
+        constexpr int S = decltype(S_)::value;  // (p - p0) & 3
+        constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
+        constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
+        __syncthreads();  // boundary rows of step p-1 are visible
+        // Row-major order: for each row k all K stages, so only one result per
+        // stage is live at a time (stage s+1 of row k needs stage s of row k
+        // only as z+; its y-neighbours are the previous step's planes in H).
+        // Stage s's result then replaces, in H, the z- plane that stage s+1 of
+        // this row has just consumed.
+#ifndef STRIP_LAZY_LDS
+        VT above[K], below[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            above[s] = *reinterpret_cast<const VT*>(&L[PR][s][wa][1][xl]);
+            below[s] = *reinterpret_cast<const VT*>(&L[PR][s][wb][0][xl]);
+        }
+#define STRIP_ABOVE(s) above[s]
+#define STRIP_BELOW(s) below[s]
+#else
+#define STRIP_ABOVE(s) (*reinterpret_cast<const VT*>(&L[PR][s][wa][1][xl]))
+#define STRIP_BELOW(s) (*reinterpret_cast<const VT*>(&L[PR][s][wb][0][xl]))
+#endif
+        bool zin[K];
+#pragma unroll
+        for (int s = 1; s <= K; ++s) {
+            const int z = p - s;
+            const int lo_s = halo_lo ? -(K - s) : 0;
+            const int hi_s = halo_hi ? nz + (K - s) : nz;
+            zin[s - 1] = z >= lo_s && z < hi_s;
+        }
+        const int zo = p - K;  // t_K(p-K) -> HBM
+        const bool do_store = DIAG != 3 && zo >= za && zo < zb;
+        char* obase = dst + int64_t(zo) * plane * int64_t(sizeof(T));
+#pragma unroll
+        for (int k = 0; k < RY; ++k) {
+            VT prev{};  // this row's result of the previous stage
+            auto stage = [&](auto s_) {
+                constexpr int s = decltype(s_)::value;
+                // t_{s-1} planes p-s (centre), p-s-1 (z-), p-s+1 (z+)
+                VT c, zm, zp, up, dn;
+                if constexpr (s == 1) {
+                    c = vin[(S + 3) & 3][k];
+                    zm = vin[(S + 2) & 3][k];
+                    zp = vin[S][k];
+                    up = k == 0 ? STRIP_ABOVE(0) : vin[(S + 3) & 3][k == 0 ? 0 : k - 1];
+                    dn = k == RY - 1 ? STRIP_BELOW(0) : vin[(S + 3) & 3][k == RY - 1 ? 0 : k + 1];
+                } else {
+                    c = H[s - 2][(S - s + 4) & 1][k];
+                    zm = H[s - 2][(S - s + 5) & 1][k];
+                    zp = prev;
+                    up = k == 0 ? STRIP_ABOVE(s - 1) : H[s - 2][(S - s + 4) & 1][k == 0 ? 0 : k - 1];
+                    dn = k == RY - 1 ? STRIP_BELOW(s - 1) : H[s - 2][(S - s + 4) & 1][k == RY - 1 ? 0 : k + 1];
+                }
+                const T wl = sdpp<kSShr1>(c[V - 1]);
+                const T er = sdpp<kSShl1>(c[0]);
+                VT o;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    T sum = (j == 0 ? wl : c[j - 1]) + (j == V - 1 ? er : c[j + 1]);
+                    sum += up[j];
+                    sum += dn[j];
+                    sum += zm[j];
+                    sum += zp[j];
+                    o[j] = DIAG == 2 ? c[j] : sfma0(sum, avg);
+                    if (s < K) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
+                }
+                // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
+                if constexpr (s >= 2) H[s - 2][(S - s + 5) & 1][k] = prev;
+                prev = o;
+            };
+            stage(std::integral_constant<int, 1>{});
+            stage(std::integral_constant<int, 2>{});
+            if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? 3 : 1)>{});
+            if constexpr (K >= 4) stage(std::integral_constant<int, (K >= 4 ? 4 : 1)>{});
+            static_assert(K >= 2 && K <= 4, "K = 2..4");
+            if (do_store && st[k]) {
+                T* q = reinterpret_cast<T*>(obase + off[k]);
+                if (xst[V - 1]) {
+                    __builtin_nontemporal_store(prev, reinterpret_cast<VT*>(q));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j)
+                        if (xst[j]) q[j] = prev[j];
+                }
+            }
+        }
+        // boundary rows for step p+1: stage 1's centre is in(p), stage s's is t_{s-1}(p-s+1)
+        if constexpr (!DB) __syncthreads();  // single buffer: every read of it is done
+        *reinterpret_cast<VT*>(&L[P][0][w][0][xl]) = vin[S][0];
+        *reinterpret_cast<VT*>(&L[P][0][w][1][xl]) = vin[S][RY - 1];
+#pragma unroll
+        for (int s = 2; s <= K; ++s) {  // t_{s-1}(p-s+1), now in H
+            *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = H[s - 2][(S - s + 5) & 1][0];
+            *reinterpret_cast<VT*>(&L[P][s - 1][w][1][xl]) = H[s - 2][(S - s + 5) & 1][RY - 1];
+        }
+        if constexpr (DIAG != 1) load_plane(vin[(S + 2) & 3], p + 2);  // slot of in(p-2), consumed above
+    };
+
+    const int plast = zb + K - 1;
+    int p = p0;
+    for (; p + 3 <= plast; p += 4) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    if (p <= plast) step(std::integral_constant<int, 0>{}, p);
+    if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
+    if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
+}
+
+int senv_int(const char* name, int dflt) {
+    const char* s = std::getenv(name);
+    return s && *s ? std::atoi(s) : dflt;
+}
+
+template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0>
+int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
+    using Tl = StripTile<T, V, RY, NW, K, DB>;
+    static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
+    const Geom g = geom_of(l);
+    const int64_t nz = end - begin;
+    if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
+    if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
+        return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
+    const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG>;
+    int zc = senv_int("STENCIL_TK_ZCHUNK", 0);
+    if (zc <= 0) {
+        // chunk count from the rounds cost model of kernels_temporalk.hip
+        static int slots = 0;
+        if (!slots) {
+            int dev = 0, cus = 0, per_cu = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
+                return set_error(STENCIL_EHIP, "occupancy query failed");
+            slots = std::max(1, cus * std::max(1, per_cu));
+        }
+        const int64_t tiles = gx * gy;
+        int64_t best_c = 1, best = INT64_MAX;
+        for (int64_t c = 1; c <= nz; ++c) {
+            const int64_t z = (nz + c - 1) / c;
+            if (c > 1 && z < 2 * K) break;
+            const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 2 * K);
+            if (cost <= best) best = cost, best_c = c;
+        }
+        zc = int((nz + best_c - 1) / best_c);
+    }
+    const int64_t gz = (nz + zc - 1) / zc;
+    const int64_t nb = gx * gy * gz;
+    if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
+    const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
+    if ((lo || hi) && l.zghost < K)
+        return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
+                         (long long)l.zghost);
+    hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
+                       static_cast<T*>(out), g, begin, end, zc, int(gx), int(gy), int(lo), int(hi),
+                       senv_int("STENCIL_TK_REMAP", 0), avg_weight<T>(l.prob));
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
+}  // namespace
+
+// cfg = RY*100 + NW (rows per wave x waves); 0 = default shape.
+int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                   int cfg, hipStream_t s) {
+    if (!temporal2_supports(l.prob))
+        return set_error(STENCIL_EUNSUPPORTED, "tkstrip supports the 3D r=1 naive 7-point star only");
+    if (l.prob.dtype == STENCIL_F32) {
+        if (steps == 3) {
+            switch (cfg) {
+            case 416: return launch_st<float, 4, 4, 16, 3, false>(l, in, out, begin, end, s);
+            case 808: return launch_st<float, 4, 8, 8, 3>(l, in, out, begin, end, s);
+            case 20808: return launch_st<float, 2, 8, 8, 3>(l, in, out, begin, end, s);
+            case 20608: return launch_st<float, 2, 6, 8, 3>(l, in, out, begin, end, s);
+            default: return launch_st<float, 4, 4, 8, 3>(l, in, out, begin, end, s);
+            }
+        }
+        if (steps == 4) {
+            switch (cfg) {
+            case 20808: return launch_st<float, 2, 8, 8, 4>(l, in, out, begin, end, s);
+            case 404: return launch_st<float, 4, 4, 8, 4>(l, in, out, begin, end, s);
+            default: return launch_st<float, 2, 7, 8, 4>(l, in, out, begin, end, s);
+            }
+        }
+    } else {
+        if (steps == 3) {
+            switch (cfg) {
+            case 416: return launch_st<double, 2, 4, 16, 3, false>(l, in, out, begin, end, s);
+            case 10408: return launch_st<double, 2, 4, 8, 3, false>(l, in, out, begin, end, s);
+            case 608: return launch_st<double, 2, 6, 8, 3>(l, in, out, begin, end, s);
+            case 216: return launch_st<double, 2, 2, 16, 3, false>(l, in, out, begin, end, s);
+            case 10808: return launch_st<double, 1, 8, 8, 3>(l, in, out, begin, end, s);
+            case 10608: return launch_st<double, 1, 6, 8, 3>(l, in, out, begin, end, s);
+            case 91: return launch_st<double, 2, 4, 8, 3, true, 1>(l, in, out, begin, end, s);
+            case 92: return launch_st<double, 2, 4, 8, 3, true, 2>(l, in, out, begin, end, s);
+            case 93: return launch_st<double, 2, 4, 8, 3, true, 3>(l, in, out, begin, end, s);
+            default: return launch_st<double, 2, 4, 8, 3>(l, in, out, begin, end, s);
+            }
+        }
+        if (steps == 4) {
+            switch (cfg) {
+            case 10808: return launch_st<double, 1, 8, 8, 4>(l, in, out, begin, end, s);
+            case 10608: return launch_st<double, 1, 6, 8, 4>(l, in, out, begin, end, s);
+            case 404: return launch_st<double, 2, 4, 8, 4>(l, in, out, begin, end, s);
+            default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
+            }
+        }
+    }
+    return set_error(STENCIL_EINVAL, "tkstrip steps must be 3 or 4 (got %d)", steps);
+}
+
+}  // namespace stencil

@@ -344,6 +344,11 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
     // x neighbours by DPP lane shifts (+6.6 % fp64 / +13 % fp32 over the LDS
     // reads of cfg 216, 512^3); 2xxxx / 3xxxx = DPP shapes (3xxxx: fp32, V = 2)
     const int cfg = env_int("STENCIL_TK_CFG", 0);
+    // Default: the strip layout (kernels_strip.hip; +2-3 % at K = 3 and the
+    // only layout whose K = 4 shapes fit the register file).  STENCIL_TK_STRIP
+    // = 0 selects this file's interleaved-row layout, > 1 a strip cfg.
+    if (const int strip = env_int("STENCIL_TK_STRIP", 1))
+        return launch_tkstrip(l, in, out, begin, end, steps, strip == 1 ? 0 : strip, s);
     if (l.prob.dtype == STENCIL_F32) {
         if (steps == 3) {
             switch (cfg) {

@@ -139,6 +139,7 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
     iteration counts leaving a remainder pair / single sweep."""
     monkeypatch.setenv("STENCIL_TK_STEPS", steps)
     monkeypatch.setenv("STENCIL_TK_ZCHUNK", zchunk)
+    monkeypatch.setenv("STENCIL_TK_STRIP", "0")  # the interleaved-row layout (kernels_temporalk.hip)
     if cfg != "default":
         monkeypatch.setenv("STENCIL_TK_CFG", cfg)
     nx, ny, nz = 131, 61, 29
@@ -149,6 +150,26 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
         assert same_bits(got, want), it
     k = int(steps)
     assert e.plan(9) == (9 // k + (9 % k) // 2 + (9 % k) % 2, 4)
+
+
+@pytest.mark.parametrize("steps,strip", [("3", "1"), ("3", "416"), ("3", "10408"), ("3", "216"), ("3", "10808"),
+                                         ("3", "20808"), ("4", "1"), ("4", "10708"), ("4", "10608"), ("4", "20708")])
+@pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])
+def test_tkstrip_chunking(gpu, monkeypatch, steps, strip, zchunk, dtype, shape3):
+    """The strip layout of the K-step kernel (kernels_strip.hip: consecutive
+    rows per wave, boundary rows through LDS): every shape, forced z-chunks,
+    remainders, grids shorter than one strip region."""
+    monkeypatch.setenv("STENCIL_TK_STEPS", steps)
+    monkeypatch.setenv("STENCIL_TK_ZCHUNK", zchunk)
+    monkeypatch.setenv("STENCIL_TK_STRIP", strip)
+    nx, ny, nz = shape3
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    for it in (3, 4, 7):
+        want = ob.run(p, it, "random", 17 + it)
+        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", "temporalk", nx, ny, nz, it, "random", 17 + it)
+        assert same_bits(got, want), it
 
 
 @pytest.mark.parametrize("cfg", ["default", "308", "216"])

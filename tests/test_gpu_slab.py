@@ -84,13 +84,17 @@ def test_slabs_bitwise_equal_single_grid(gpu, world, fused, split, shape):
 @pytest.mark.parametrize("shape,k", [("star", 3), ("star", 4), ("box", 2), ("box", 3)])
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("cfg", ["default", "312"])
+@pytest.mark.parametrize("cfg", ["default", "312", "strip1"])
 def test_slabs_k_step_rounds(gpu, monkeypatch, world, shape, k, split, cfg):
-    """k fused sweeps per k-plane halo exchange (TEMPORALK / the K-step box
-    kernel with HALO_LO/HI): halo planes advanced to t+k-1 .. t+1 inside the
-    launch."""
-    if cfg != "default":
+    """k fused sweeps per k-plane halo exchange (TEMPORALK -- strip layout by
+    default, the interleaved-row layout with cfg 312, the strip default shape
+    for the other K -- and the K-step box kernel with HALO_LO/HI): halo planes
+    advanced to t+k-1 .. t+1 inside the launch."""
+    if cfg == "312":
+        monkeypatch.setenv("STENCIL_TK_STRIP", "0")
         monkeypatch.setenv("STENCIL_TK_CFG", cfg)
+    elif cfg == "strip1":
+        monkeypatch.setenv("STENCIL_TK_STRIP", "404" if k == 4 else "10808")
     monkeypatch.setenv("STENCIL_TK_ZCHUNK", "5")
     monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", "5")
     nx, ny, nz, it = 70, 45, 29, 11

@@ -19,9 +19,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("temporalk_7pt", "temporal2_7pt", "zmarch7", "sweep_direct", "copy_kernel", "fill_initial_kernel", "plane_sums"):
+    """Kernel family name as bench.py reports it."""
+    table = (("tkstrip_7pt", "temporalk"), ("temporalk_7pt", "temporalk"), ("temporal2_7pt", "temporal2"),
+             ("zmarch7", "zmarch"), ("sweep_direct", "direct"), ("boxk_27pt", "boxk"), ("box27_zmarch", "box27"),
+             ("copy_kernel", "copy_kernel"), ("fill_initial_kernel", "fill_initial_kernel"),
+             ("plane_sums", "plane_sums"))
+    for k, v in table:
         if k in name:
-            return k.replace("_7pt", "").replace("7", "") if k != "copy_kernel" else k
+            return v
     return name[:40]
 
 
