@@ -80,8 +80,8 @@ struct StripTile {
 // first two planes, 2 = no arithmetic (t_s = centre), 3 = no stores
 template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0>
 __global__ void __launch_bounds__(64 * NW)
-    tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend, int zchunk,
-                int tiles_x, int tiles_y, int halo_lo, int halo_hi, int remap, T avg) {
+    tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
+                int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -89,21 +89,25 @@ __global__ void __launch_bounds__(64 * NW)
     static_assert(RY >= 2, "a strip needs a first and a last row");
     __shared__ __attribute__((aligned(16))) T L[NB][K][NW][2][RW];
 
-    int t = blockIdx.x;
-    if (remap) {  // XCD j gets the j-th contiguous run of tiles (see kernels_temporalk.hip)
-        const int nb = gridDim.x, q = nb >> 3, r8 = nb & 7, j = t & 7;
-        t = j * q + (j < r8 ? j : r8) + (t >> 3);
+    // Work = the linearised (tile, z) space of the range, tile-major: units
+    // [lo, hi) of it per workgroup.  zchunk > 0: fixed chunks of every tile;
+    // zchunk == 0: one equal share per workgroup (the grid is one workgroup
+    // per slot), walked as one segment per tile it touches -- no partial last
+    // round, at the price of one extra pipeline fill per segment boundary.
+    const int nzr = zend - zbeg;
+    const int64_t tiles = int64_t(tiles_x) * tiles_y;
+    int64_t lo, hi;
+    if (zchunk > 0) {
+        const int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
+        lo = t * nzr + c * zchunk;
+        hi = lo + (zchunk < nzr - c * zchunk ? zchunk : nzr - c * zchunk);
+    } else {
+        const int64_t units = tiles * nzr;
+        lo = units * blockIdx.x / gridDim.x;
+        hi = units * (blockIdx.x + 1) / gridDim.x;
     }
-    const int bx = t % tiles_x;
-    const int by = (t / tiles_x) % tiles_y;
-    const int bz = t / (tiles_x * tiles_y);
 
     const int lane = threadIdx.x, w = threadIdx.y;
-    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
-    const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
-    // z bookkeeping in 32 bits (nz < 2^31, checked at launch) so it stays scalar
-    const int za = int(zbeg) + bz * zchunk;
-    const int zb = za + zchunk < int(zend) ? za + zchunk : int(zend);
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
     // Addresses are a uniform per-plane base (SGPRs) + a non-negative 32-bit
@@ -119,6 +123,20 @@ __global__ void __launch_bounds__(64 * NW)
         VT* l16 = reinterpret_cast<VT*>(&L[0][0][0][0][0]);
         for (int i = threadIdx.y * 64 + threadIdx.x; i < N16; i += 64 * NW) l16[i] = VT{};
     }
+
+    const int xl = lane * V;
+    // neighbour strips (the first / last wave reads its own: those rows are ring rows)
+    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+
+    while (lo < hi) {  // one segment: tile t, planes [za, zb)
+    const int t = int(lo / nzr);
+    const int za = zbeg + int(lo - int64_t(t) * nzr);
+    const int zb = za + (hi - lo < int64_t(zend - za) ? int(hi - lo) : zend - za);
+    lo += zb - za;
+    const int bx = t % tiles_x;
+    const int by = t / tiles_x;
+    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
+    const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
 
     // Unconditional loads from clamped addresses (kernels_temporalk.hip): the
     // plane wait is then a counted vmcnt, not vmcnt(0).
@@ -167,9 +185,6 @@ __global__ void __launch_bounds__(64 * NW)
     load_plane(vin[0], p0);
     load_plane(vin[1], p0 + 1);
 
-    const int xl = lane * V;
-    // neighbour strips (the first / last wave reads its own: those rows are ring rows)
-    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
 
     auto step = [&](auto S_, int p) {
         constexpr int S = decltype(S_)::value;  // (p - p0) & 3
@@ -181,19 +196,9 @@ __global__ void __launch_bounds__(64 * NW)
         // only as z+; its y-neighbours are the previous step's planes in H).
         // Stage s's result then replaces, in H, the z- plane that stage s+1 of
         // this row has just consumed.
-#ifndef STRIP_LAZY_LDS
-        VT above[K], below[K];
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-            above[s] = *reinterpret_cast<const VT*>(&L[PR][s][wa][1][xl]);
-            below[s] = *reinterpret_cast<const VT*>(&L[PR][s][wb][0][xl]);
-        }
-#define STRIP_ABOVE(s) above[s]
-#define STRIP_BELOW(s) below[s]
-#else
+        // the neighbour strips' boundary rows, read where used (row 0 / RY-1)
 #define STRIP_ABOVE(s) (*reinterpret_cast<const VT*>(&L[PR][s][wa][1][xl]))
 #define STRIP_BELOW(s) (*reinterpret_cast<const VT*>(&L[PR][s][wb][0][xl]))
-#endif
         bool zin[K];
 #pragma unroll
         for (int s = 1; s <= K; ++s) {
@@ -281,6 +286,7 @@ __global__ void __launch_bounds__(64 * NW)
     if (p <= plast) step(std::integral_constant<int, 0>{}, p);
     if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
     if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
+    }  // segments
 }
 
 int senv_int(const char* name, int dflt) {
@@ -299,9 +305,12 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
     auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG>;
+    const int64_t tiles = gx * gy;
     int zc = senv_int("STENCIL_TK_ZCHUNK", 0);
-    if (zc <= 0) {
-        // chunk count from the rounds cost model of kernels_temporalk.hip
+    int64_t nb = 0;
+    if (zc > 0) {
+        nb = tiles * ((nz + zc - 1) / zc);  // fixed chunks (tests: seams, short chunks)
+    } else {
         static int slots = 0;
         if (!slots) {
             int dev = 0, cus = 0, per_cu = 0;
@@ -311,26 +320,37 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
                 return set_error(STENCIL_EHIP, "occupancy query failed");
             slots = std::max(1, cus * std::max(1, per_cu));
         }
-        const int64_t tiles = gx * gy;
-        int64_t best_c = 1, best = INT64_MAX;
-        for (int64_t c = 1; c <= nz; ++c) {
-            const int64_t z = (nz + c - 1) / c;
-            if (c > 1 && z < 2 * K) break;
-            const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 2 * K);
-            if (cost <= best) best = cost, best_c = c;
+        if (senv_int("STENCIL_TK_BALANCE", 0)) {
+            // one equal share of the (tile, z) units per slot, each share at
+            // least 4K planes long (a segment costs 2K planes of pipeline fill).
+            // Measured 20-30 % SLOWER than whole chunks on MI355X (512^3 fp64
+            // 902 vs 1120 Gcell/s, 2048^2 x 512 984 vs 1386): the shares start
+            // at scattered z, so x/y-neighbour tiles no longer read their
+            // shared halo lines at about the same time and those re-reads miss
+            // L2 / Infinity Cache.  Chunk rounds keep all tiles of a chunk in
+            // z lock-step.
+            nb = std::max<int64_t>(1, std::min<int64_t>(slots, tiles * nz / (4 * K)));
+        } else {
+            // whole chunks: the count minimising rounds x (chunk + 2K)
+            int64_t best_c = 1, best = INT64_MAX;
+            for (int64_t c = 1; c <= nz; ++c) {
+                const int64_t z = (nz + c - 1) / c;
+                if (c > 1 && z < 2 * K) break;
+                const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 2 * K);
+                if (cost <= best) best = cost, best_c = c;
+            }
+            zc = int((nz + best_c - 1) / best_c);
+            nb = tiles * ((nz + zc - 1) / zc);
         }
-        zc = int((nz + best_c - 1) / best_c);
     }
-    const int64_t gz = (nz + zc - 1) / zc;
-    const int64_t nb = gx * gy * gz;
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
     const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
     if ((lo || hi) && l.zghost < K)
         return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
                          (long long)l.zghost);
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
-                       static_cast<T*>(out), g, begin, end, zc, int(gx), int(gy), int(lo), int(hi),
-                       senv_int("STENCIL_TK_REMAP", 0), avg_weight<T>(l.prob));
+                       static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
+                       avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
