@@ -96,7 +96,7 @@ enum {
     STENCIL_KERNEL_DIRECT = 1,    /* one cell per lane, neighbours via L1/L2 */
     STENCIL_KERNEL_ZMARCH = 2,    /* 2.5D: LDS plane + z register queue */
     STENCIL_KERNEL_TEMPORAL2 = 3, /* ZMARCH with 2 fused time steps per launch */
-    STENCIL_KERNEL_TEMPORALK = 4  /* 3D 7-point star: K = 3 or 4 fused steps per launch
+    STENCIL_KERNEL_TEMPORALK = 4  /* 3D 7-point star: K = 3..5 fused steps per launch
                                      (K = env STENCIL_TK_STEPS, default 4) */
 };
 enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
@@ -178,7 +178,7 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
                    void* stream);
 
 /* K fused sweeps, out = S^K(in) on [begin, end): steps 1 = stencil_sweep,
- * 2 = stencil_sweep2, 3 or 4 = the TEMPORALK kernel (3D 7-point star), 3 =
+ * 2 = stencil_sweep2, 3..5 = the TEMPORALK kernel (3D 7-point star), 3 =
  * the K-step box kernel (3D 27-point box; kernels_boxk.hip, which also serves
  * the box's 2-step sweep2).
  * With HALO_LO/HI flags the grid needs halo >= steps. */

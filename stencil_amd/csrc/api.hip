@@ -89,10 +89,12 @@ bool iterate_fused(const stencil_problem& p) {
 }
 
 // Steps per launch of the deep temporal-blocking family (kernels_strip.hip,
-// kernels_temporalk.hip) in stencil_iterate: K = STENCIL_TK_STEPS (3 or 4,
-// default 4) for explicit
-// TEMPORALK and for AUTO on the 7-point star (STENCIL_NO_TK=1 or
-// STENCIL_NO_T2=1 turn the latter off); 0 = not used.
+// kernels_temporalk.hip) in stencil_iterate, for explicit TEMPORALK and for
+// AUTO on the 7-point star (STENCIL_NO_TK=1 or STENCIL_NO_T2=1 turn the
+// latter off); 0 = not used.  K = STENCIL_TK_STEPS (3, 4 or 5), else the
+// measured best (MI355X, tools/strip_ab.sh): 4 for fp64 (5: -3 % at 512^3,
+// -5 % at 2048^2 x 512) and for small fp32 planes, 5 for fp32 planes of
+// >= 1024^2 cells (+24 % at 2048^2 x 512, -9 % at 512^3).
 int iterate_tk_steps(const stencil_problem& p) {
     if (!temporal2_supports(p)) return 0;
     if (p.kernel == STENCIL_KERNEL_AUTO) {
@@ -103,8 +105,8 @@ int iterate_tk_steps(const stencil_problem& p) {
         return 0;
     }
     const char* k = std::getenv("STENCIL_TK_STEPS");
-    const int steps = k && *k ? std::atoi(k) : 4;
-    return steps == 3 || steps == 4 ? steps : 0;
+    const int steps = k && *k ? std::atoi(k) : (p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4);
+    return steps >= 3 && steps <= 5 ? steps : 0;
 }
 
 // 2D problems iterate K sweeps per launch with the tile resident in LDS
@@ -400,7 +402,7 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
     if (steps == 1) return stencil_sweep(l, in, out, begin, end, stream);
     if (steps == 2) return stencil_sweep2(l, in, out, begin, end, stream);
     if (int rc = check_layout(l)) return rc;
-    if (steps != 3 && steps != 4) return set_error(STENCIL_EINVAL, "steps must be 1..4 (got %d)", steps);
+    if (steps < 3 || steps > 5) return set_error(STENCIL_EINVAL, "steps must be 1..5 (got %d)", steps);
     const bool box = box27_supports(l->prob);
     if (!temporal2_supports(l->prob) && !(box && steps == 3))
         return set_error(STENCIL_EUNSUPPORTED,

@@ -251,7 +251,9 @@ __global__ void __launch_bounds__(64 * NW)
             stage(std::integral_constant<int, 2>{});
             if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? 3 : 1)>{});
             if constexpr (K >= 4) stage(std::integral_constant<int, (K >= 4 ? 4 : 1)>{});
-            static_assert(K >= 2 && K <= 4, "K = 2..4");
+            if constexpr (K >= 5) stage(std::integral_constant<int, (K >= 5 ? 5 : 1)>{});
+            if constexpr (K >= 6) stage(std::integral_constant<int, (K >= 6 ? 6 : 1)>{});
+            static_assert(K >= 2 && K <= 6, "K = 2..6");
             if (do_store && st[k]) {
                 T* q = reinterpret_cast<T*>(obase + off[k]);
                 if (xst[V - 1]) {
@@ -403,7 +405,19 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             }
         }
     }
-    return set_error(STENCIL_EINVAL, "tkstrip steps must be 3 or 4 (got %d)", steps);
+    if (steps == 5) {
+        if (l.prob.dtype == STENCIL_F32) {
+            switch (cfg) {
+            case 20608: return launch_st<float, 2, 6, 8, 5>(l, in, out, begin, end, s);
+            default: return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
+            }
+        }
+        switch (cfg) {
+        case 10608: return launch_st<double, 1, 6, 8, 5>(l, in, out, begin, end, s);
+        default: return launch_st<double, 1, 5, 8, 5>(l, in, out, begin, end, s);
+        }
+    }
+    return set_error(STENCIL_EINVAL, "tkstrip steps must be 3, 4 or 5 (got %d)", steps);
 }
 
 }  // namespace stencil

@@ -390,7 +390,8 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
             }
         }
     }
-    return set_error(STENCIL_EINVAL, "temporalk steps must be 3 or 4 (got %d)", steps);
+    return set_error(STENCIL_EINVAL, "the interleaved-row temporalk layout does %s steps; 3 or 4 only (got %d)",
+                     steps == 5 ? "not do 5" : "not do these", steps);
 }
 
 }  // namespace stencil

@@ -111,7 +111,7 @@ class JacobiEngine:
                    "stencil_sweep2")
 
     def sweepk(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int, stream=None) -> None:
-        """dst = S^steps(src) on [begin, end) in one launch (steps 1..4)."""
+        """dst = S^steps(src) on [begin, end) in one launch (steps 1..5; box: 1..3)."""
         _lib.check(self.lib.stencil_sweepk(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
                                            _stream_handle(stream)), "stencil_sweepk")

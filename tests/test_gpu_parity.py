@@ -153,7 +153,8 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
 
 
 @pytest.mark.parametrize("steps,strip", [("3", "1"), ("3", "416"), ("3", "10408"), ("3", "216"), ("3", "10808"),
-                                         ("3", "20808"), ("4", "1"), ("4", "10708"), ("4", "10608"), ("4", "20708")])
+                                         ("3", "20808"), ("4", "1"), ("4", "10708"), ("4", "10608"), ("4", "20708"),
+                                         ("5", "1"), ("5", "10608"), ("5", "20608")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])
