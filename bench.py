@@ -50,19 +50,32 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n: int, budget_s: float):
+def host_threads() -> int:
+    """The host cores this process may use (the GPU box's CPU share: its
+    OMP_NUM_THREADS, else the affinity mask)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(env))) if env.isdigit() and int(env) > 0 else n
+
+
+def cpu_baseline(n: int, budget_s: float, threads: int = 1):
     """The oracle (port of check_result's loop, stencil.cpp:94-131, generalised
-    to 3D) on the host, single-threaded like the reference, over a bounded
-    number of sweeps of the same 512^3 fp64 grid."""
+    to 3D) on the host over a bounded number of sweeps of the same 512^3 fp64
+    grid: single-threaded like the reference's own CPU path, or with OpenMP
+    over `threads` cores (identical per-cell arithmetic, bitwise-equal result)."""
     from oracle import binding as ob
     p = ob.problem(3, "fp64", "star", 1, "naive", n, n, n)
-    t1 = ob.timed_run(p, 1, threads=1)
+    t1 = ob.timed_run(p, 1, threads=threads)
     iters = max(1, min(200, int(budget_s / max(t1, 1e-6))))
-    t = ob.timed_run(p, iters, threads=1)
+    t = ob.timed_run(p, iters, threads=threads)
     cells = float(n) ** 3 * iters
-    return {"value": round(cells / t / 1e9, 4), "unit": "Gcell-updates/s", "cores": 1, "kind": "port",
+    who = "1 host thread" if threads == 1 else f"{threads} host threads (OpenMP)"
+    return {"value": round(cells / t / 1e9, 4), "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ naive sweep, {n}^3 fp64 7-point, {iters} sweeps from the reference initial "
-                      f"condition, {t:.1f} s on 1 host thread"}
+                      f"condition, {t:.1f} s on {who}"}
 
 
 def load_traffic(workload_key: str, kernel_name: str):
@@ -209,6 +222,8 @@ def main():
             out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+            # the same loop with OpenMP over the host's cores too
+            out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads())
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "common.hpp"
 
@@ -549,7 +550,7 @@ int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, 
 // never written.  Here: both host grids go to HBM, the GPU sweeps, the final
 // grid comes back into the parity-selected host buffer.
 // ---------------------------------------------------------------------------
-static void reference_entry(StencilArguments* args, int order) {
+static void reference_entry(StencilArguments* args, int order, bool rma) {
     clear_error();
     if (!args) { set_error(STENCIL_EINVAL, "null arguments"); return; }
     const StencilMatrixView& in = args->input;
@@ -563,47 +564,77 @@ static void reference_entry(StencilArguments* args, int order) {
         set_error(STENCIL_EINVAL, "input and output views differ in shape");
         return;
     }
-    const int r = int(in.boundary_width);
+    const int64_t r = int64_t(in.boundary_width);
     if (in.actual_width < size_t(2 * r) || in.actual_height < size_t(2 * r)) {
         set_error(STENCIL_EINVAL, "view smaller than its ghost ring");
         return;
     }
+    const int64_t nx = int64_t(in.actual_width) - 2 * r, ny = int64_t(in.actual_height) - 2 * r;
+    // The 64 workers take blocks (ROW, COL) in 0..7 of block_size^2 cells,
+    // clipped at the edge; a block past the edge is empty and its worker
+    // returns (block_subview, boundary_matrix.hpp:190-218; stencil_dma.cpp:
+    // 404-415).  So only [0, 8b)^2 is ever computed: cells at or past 8b keep
+    // their initial value and feed the computed ones as fixed neighbours.
+    const int64_t reach = 8 * int64_t(args->block_size);
+    const int64_t ex = std::min(nx, reach), ey = std::min(ny, reach);
+    if (ex == 0 || ey == 0) return;
     stencil_problem p{};
     p.dims = 2;
     p.dtype = STENCIL_F32;
     p.shape = STENCIL_STAR;
-    p.radius = r;
+    p.radius = int(r);
     p.order = order;
     p.kernel = STENCIL_KERNEL_AUTO;
-    p.nx = int64_t(in.actual_width) - 2 * r;
-    p.ny = int64_t(in.actual_height) - 2 * r;
+    p.nx = ex;
+    p.ny = ey;
     p.nz = 1;
-    if (p.nx == 0 || p.ny == 0) return;  // empty blocks return silently (stencil_dma.cpp:413-415)
     stencil_layout l;
     if (stencil_layout_init(&p, &l)) return;
+    // Host staging of the computed sub-view incl. its ghost ring.  RMA does
+    // not read ghosts: block column 7 / row 7 synthesise x-faces = 1 and
+    // y-faces = 0 (stencil_rma.cpp:149-166), which differs from the host
+    // cells at 8b when n > 8b.
+    const int64_t hw = ex + 2 * r, hh = ey + 2 * r, stride = int64_t(in.data_stride);
+    std::vector<float> ha(size_t(hw * hh)), hb(size_t(hw * hh));
+    for (int64_t y = 0; y < hh; ++y) {
+        std::memcpy(&ha[size_t(y * hw)], in.data + y * stride, size_t(hw) * sizeof(float));
+        std::memcpy(&hb[size_t(y * hw)], out.data + y * stride, size_t(hw) * sizeof(float));
+    }
+    if (rma) {
+        for (std::vector<float>* h : {&ha, &hb}) {
+            if (ex < nx)
+                for (int64_t y = r; y < ey + r; ++y) (*h)[size_t(y * hw + ex + r)] = 1.f;
+            if (ey < ny)
+                for (int64_t x = r; x < ex + r; ++x) (*h)[size_t((ey + r) * hw + x)] = 0.f;
+        }
+    }
     void* a = nullptr;
     void* b = nullptr;
     if (stencil_alloc(&l, &a)) return;
     if (stencil_alloc(&l, &b)) { (void)hipFree(a); return; }
     int final_in_b = 0;
-    int rc = stencil_upload(&l, a, in.data, int64_t(in.data_stride), int64_t(in.actual_height), nullptr);
-    if (!rc) rc = stencil_upload(&l, b, out.data, int64_t(out.data_stride), int64_t(out.actual_height), nullptr);
+    int rc = stencil_upload(&l, a, ha.data(), hw, hh, nullptr);
+    if (!rc) rc = stencil_upload(&l, b, hb.data(), hw, hh, nullptr);
     if (!rc) rc = stencil_iterate(&l, a, b, args->iterations, nullptr, &final_in_b, nullptr);
-    if (!rc) {
-        const StencilMatrixView& dst = (args->iterations & 1u) ? out : in;
-        rc = stencil_download(&l, final_in_b ? b : a, dst.data, int64_t(dst.data_stride), int64_t(dst.actual_height), nullptr);
-    }
+    if (!rc) rc = stencil_download(&l, final_in_b ? b : a, ha.data(), hw, hh, nullptr);
     if (!rc) {
         hipError_t e = hipStreamSynchronize(nullptr);
-        if (e != hipSuccess) set_error(STENCIL_EHIP, "synchronize: %s", hipGetErrorString(e));
+        if (e != hipSuccess) rc = set_error(STENCIL_EHIP, "synchronize: %s", hipGetErrorString(e));
+    }
+    if (!rc) {
+        // only the computed interior is written back: ghost cells are never
+        // written (stencil_dma.cpp puts block interiors only)
+        const StencilMatrixView& dst = (args->iterations & 1u) ? out : in;
+        for (int64_t y = r; y < ey + r; ++y)
+            std::memcpy(dst.data + y * stride + r, &ha[size_t(y * hw + r)], size_t(ex) * sizeof(float));
     }
     (void)hipFree(a);
     (void)hipFree(b);
 }
 
-void stencil_iterate_dma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
-void stencil_iterate_dma_static_unroll(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_NAIVE); }
-void stencil_iterate_dma_slave_pack(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
-void stencil_iterate_rma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA); }
+void stencil_iterate_dma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA, false); }
+void stencil_iterate_dma_static_unroll(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_NAIVE, false); }
+void stencil_iterate_dma_slave_pack(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA, false); }
+void stencil_iterate_rma(StencilArguments* args) { reference_entry(args, STENCIL_ORDER_DMA, true); }
 
 }  // extern "C"

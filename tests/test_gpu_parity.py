@@ -358,6 +358,57 @@ def test_reference_abi_entry_points(gpu, fn, order, n, it, r):
     assert same_bits(got, ob.run(p, it))
 
 
+def _reference_block_reach(a, it, r, order, ex, ey, rma):
+    """What the reference computes when only blocks (ROW, COL) in 0..7 of b^2
+    cells exist (boundary_matrix.hpp:190-218): the [0, 8b)^2 sub-grid, whose
+    x = 8b / y = 8b neighbours are the untouched host cells -- or, for RMA,
+    synthesised Dirichlet faces 1 / 0 (stencil_rma.cpp:149-166).  Cells past
+    8b keep their initial value.  Oracle sweeps on the sub-array."""
+    n = a.shape[0] - 2 * r
+    sub = a[:ey + 2 * r, :ex + 2 * r].copy()
+    if rma:
+        if ex < n:
+            sub[r:ey + r, ex + r] = 1
+        if ey < n:
+            sub[ey + r, r:ex + r] = 0
+    ps = ob.problem(2, "fp32", "star", r, order, ex, ey)
+    A, B = sub.copy(), sub.copy()
+    for _ in range(it):
+        ob.sweep(ps, A, B, 0, ey)
+        A, B = B, A
+    full = a.copy()
+    full[r:ey + r, r:ex + r] = A[r:ey + r, r:ex + r]
+    return full
+
+
+@pytest.mark.parametrize("fn,order,rma", [("stencil_iterate_dma", "dma", False),
+                                          ("stencil_iterate_dma_static_unroll", "naive", False),
+                                          ("stencil_iterate_dma_slave_pack", "dma", False),
+                                          ("stencil_iterate_rma", "dma", True)])
+@pytest.mark.parametrize("n,b,it", [(80, 8, 9), (100, 10, 4), (64, 8, 5), (70, 9, 6), (40, 0, 3)])
+def test_reference_abi_block_reach(gpu, fn, order, rma, n, b, it):
+    """-s n -b b with n > 8b: the reference never computes rows / columns at
+    or past 8b; block_size 0 computes nothing."""
+    from stencil_amd import _lib
+    lib = _lib.load()
+    r = 1
+    p = ob.problem(2, "fp32", "star", r, order, n, n)
+    a = ob.init(p, "random", 3)
+    a0 = a.copy()
+    bb = a.copy()
+    def view(arr):
+        return _lib.MatrixView(n + 2 * r, n + 2 * r, r, r, n + 2 * r, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    args = _lib.Arguments(b, it, view(a), view(bb))
+    getattr(lib, fn)(ctypes.byref(args))
+    assert lib.stencil_last_error() == 0, lib.stencil_last_error_message()
+    got = bb if it % 2 else a
+    reach = min(n, 8 * b)
+    want = a0 if reach == 0 else _reference_block_reach(a0, it, r, order, reach, reach, rma)
+    assert same_bits(got, want)
+    other = a if it % 2 else bb  # the other buffer: the reference leaves it holding some earlier sweep;
+    assert same_bits(other[reach + r:], a0[reach + r:])  # its never-computed rows stay initial
+
+
 # ----------------------------------------------------------------- CLI
 def test_cli_check_result_on_gpu(gpu):
     cli = os.path.join(ROOT, "build", "bin", "stencil_main")
@@ -373,6 +424,22 @@ def test_cli_check_result_on_gpu(gpu):
                          timeout=300)
     assert out.returncode == 0, out.stderr + out.stdout
     assert out.stdout.count("is correct.") == 3
+
+
+def test_cli_block_reach(gpu):
+    """-s 80 -b 8: the reference methods compute only [0, 64)^2, so their
+    check_result fails exactly like the reference's (main.cpp:17-22: the
+    "incorrect" line, no timing lines); the GPU-native HIP method computes
+    the whole grid."""
+    cli = os.path.join(ROOT, "build", "bin", "stencil_main")
+    out = subprocess.run([cli, "-s", "80", "-b", "8", "-i", "20", "-m", "DMA", "RMA", "HIP", "-c"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 3, out.stderr  # extension: a failed check is a non-zero exit (the reference exits 0)
+    for m in ("DMA", "RMA"):
+        assert f"The results of method {m} is incorrect." in out.stdout
+        assert f"The average time taken by {m} method" not in out.stdout
+    assert "The results of method HIP is correct." in out.stdout
+    assert out.stdout.count("invalid result at (") == 2
 
 
 def test_cli_bmp_dump(gpu, tmp_path):
