@@ -30,6 +30,31 @@ CONFIGS = {
 }
 
 
+# CPU baseline per config: the oracle's naive sweep on the
+# host, single-threaded (the reference's CPU path) and with OpenMP over the
+# host's CPU share; full size where that fits a ~10 s budget, else the rate
+# on a 512^3 sub-problem of the same stencil and dtype.
+CPU_SAMPLE = {"C1": (1024, 1024, 1), "C1r": (1024, 1024, 1), "C2": (512, 512, 512), "C3r": (512, 512, 512),
+              "C4s": (512, 512, 512), "C5s": (512, 512, 512)}
+
+
+def cpu_rate(name, c, budget_s=8.0):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import host_threads
+    from oracle import binding as ob
+    spec = c["spec"]
+    nx, ny, nz = CPU_SAMPLE[name]
+    p = ob.problem(spec.dims, spec.dtype, spec.shape, spec.radius, spec.order, nx, ny, nz)
+    out = {}
+    for threads in (1, host_threads()):
+        t1 = ob.timed_run(p, 1, threads=threads)
+        it = max(1, min(c["iters"], int(budget_s / max(t1, 1e-6))))
+        t = ob.timed_run(p, it, threads=threads)
+        out[f"threads_{threads}"] = {"gcell_per_s": round(nx * ny * nz * it / t / 1e9, 4), "iterations": it,
+                                     "grid": [nx, ny, nz], "seconds": round(t, 2)}
+    return out
+
+
 def run(name, c):
     spec, (nx, ny, nz), iters = c["spec"], c["shape"], c["iters"]
     e = JacobiEngine(spec, nx, ny, nz)
@@ -48,6 +73,10 @@ def run(name, c):
            "alg_GBps": round(cells * iters * 2 * spec.elem_bytes / (dev_ms * 1e-3) / 1e9, 1)}
     del e
     torch.cuda.empty_cache()
+    if os.environ.get("CONFIGS_CPU", "1") != "0":
+        out["cpu_baseline"] = cpu_rate(name, c)
+        best = max(v["gcell_per_s"] for v in out["cpu_baseline"].values())
+        out["gpu_over_best_cpu"] = round(out["gcell_per_s"] / best, 1)
     return out
 
 
