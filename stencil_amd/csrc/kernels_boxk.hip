@@ -71,7 +71,10 @@ struct BKTile {
     static constexpr size_t lds_bytes = size_t(K) * LY * LX * sizeof(T);
 };
 
-template <typename T, int V, int RY, int NW, int K, int R>
+// XD: x-neighbours by DPP lane shifts (true, default) or by two extra LDS
+// reads per row (false; measured 11-13 % slower in fp64 although the DPP
+// moves are ~18 % of the kernel's VALU instructions).
+template <typename T, int V, int RY, int NW, int K, int R, bool XD>
 __global__ void __launch_bounds__(64 * NW)
     boxk_27pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend, int zchunk,
               int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
@@ -89,11 +92,16 @@ __global__ void __launch_bounds__(64 * NW)
     const int lane = threadIdx.x, w = threadIdx.y;
     const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
     const int64_t y0 = int64_t(by) * TY - K;
-    const int64_t za = zbeg + int64_t(bz) * zchunk;
-    const int64_t zb = za + zchunk < zend ? za + zchunk : zend;
-    const T* __restrict__ src = in + g.origin;
-    T* __restrict__ dst = out + g.origin;
+    // z in 32-bit scalars; addresses = uniform per-plane base + one
+    // non-negative 32-bit byte offset per row (saddr form), as in
+    // kernels_strip.hip
+    const int za = int(zbeg) + bz * zchunk;
+    const int zb = za + zchunk < int(zend) ? za + zchunk : int(zend);
+    const int nz = int(g.nz);
     const int64_t plane = g.plane;
+    const int64_t bias = g.row + XR * V;
+    const char* __restrict__ src = reinterpret_cast<const char*>(in + g.origin - bias);
+    char* __restrict__ dst = reinterpret_cast<char*>(out + g.origin - bias);
 
     {
         constexpr int N16 = int(Tl::lds_bytes / 16);
@@ -102,7 +110,7 @@ __global__ void __launch_bounds__(64 * NW)
     }
 
     // unconditional loads from clamped addresses (see kernels_temporalk.hip)
-    int off[RY];
+    uint32_t off[RY];
     bool yin[RY], st[RY];
     const int64_t xmax = g.nx / V * V;
     const int64_t xc = x < xmax ? x : xmax;
@@ -111,7 +119,7 @@ __global__ void __launch_bounds__(64 * NW)
         const int rr = w + NW * k;
         const int64_t y = y0 + rr;
         const int64_t yc = y < -1 ? -1 : (y > g.ny ? g.ny : y);
-        off[k] = int(yc * g.row + xc);
+        off[k] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
         yin[k] = y >= 0 && y < g.ny;
         st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < 64 - XR;
     }
@@ -121,17 +129,17 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
-    const int64_t ld_lo = halo_lo ? -K : -1;
-    const int64_t ld_hi = halo_hi ? g.nz + K - 1 : g.nz;
-    const int64_t zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
-    auto load_plane = [&](VT (&d)[RY], int64_t z) {
-        const int64_t zz = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
-        const T* base = src + zz * plane;
+    const int ld_lo = halo_lo ? -K : -1;
+    const int ld_hi = halo_hi ? nz + K - 1 : nz;
+    const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
+    auto load_plane = [&](VT (&d)[RY], int z) {
+        const int zz = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
+        const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
-        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + int64_t(off[k]));
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
     };
 
-    const int64_t p0 = za - K;
+    const int p0 = za - K;
     VT vin[R][RY];
     VT part[2][K][RY];  // running sums, parity-indexed: [P^1] = t_s(q-1) (finish), [P] = t_s(q) (continue)
     VT cen[2][K][RY];   // own centre of the stage's input plane, parity-indexed ([P^1] = plane q-1)
@@ -148,16 +156,16 @@ __global__ void __launch_bounds__(64 * NW)
     for (int i = 0; i < R; ++i) load_plane(vin[i], p0 + i);
     const int xx = V + lane * V;
 
-    auto step = [&](auto S_, int64_t p) {
+    auto step = [&](auto S_, int p) {
         constexpr int S = decltype(S_)::value;
         constexpr int P = S & 1;
         __syncthreads();  // A
         VT res[K][RY];
 #pragma unroll
         for (int s = 1; s <= K; ++s) {
-            const int64_t m = p - 2 * s;  // plane finished now
-            const int64_t lo_s = halo_lo ? -(K - s) : 0;
-            const int64_t hi_s = halo_hi ? g.nz + (K - s) : g.nz;
+            const int m = p - 2 * s;  // plane finished now
+            const int lo_s = halo_lo ? -(K - s) : 0;
+            const int hi_s = halo_hi ? nz + (K - s) : nz;
             const bool zin = m >= lo_s && m < hi_s;
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
@@ -167,10 +175,18 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
                 for (int r = 0; r < 3; ++r) {
                     const VT c = *reinterpret_cast<const VT*>(&L[s - 1][yy - 1 + r][xx]);
-                    nb[r][0] = bdpp<kShr1>(c[V - 1]);
+                    if constexpr (XD) {
+                        nb[r][0] = bdpp<kShr1>(c[V - 1]);
+                    } else {
+                        nb[r][0] = L[s - 1][yy - 1 + r][xx - 1];
+                    }
 #pragma unroll
                     for (int j = 0; j < V; ++j) nb[r][j + 1] = c[j];
-                    nb[r][V + 1] = bdpp<kShl1>(c[0]);
+                    if constexpr (XD) {
+                        nb[r][V + 1] = bdpp<kShl1>(c[0]);
+                    } else {
+                        nb[r][V + 1] = L[s - 1][yy - 1 + r][xx + V];
+                    }
                 }
                 VT fin, cont, start, o;
 #pragma unroll
@@ -215,12 +231,13 @@ __global__ void __launch_bounds__(64 * NW)
 #endif
         }
         // t_K(p-2K) -> HBM
-        const int64_t zo = p - 2 * K;
+        const int zo = p - 2 * K;
         if (zo >= za && zo < zb) {
+            char* obase = dst + int64_t(zo) * plane * int64_t(sizeof(T));
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
                 if (st[k]) {
-                    T* q = dst + zo * plane + int64_t(off[k]);
+                    T* q = reinterpret_cast<T*>(obase + off[k]);
                     if (xst[V - 1]) {
                         __builtin_nontemporal_store(res[K - 1][k], reinterpret_cast<VT*>(q));
                     } else {
@@ -242,8 +259,8 @@ __global__ void __launch_bounds__(64 * NW)
         load_plane(vin[S], p + R);
     };
 
-    const int64_t plast = zb - 1 + 2 * K;
-    int64_t p = p0;
+    const int plast = zb - 1 + 2 * K;
+    int p = p0;
     for (; p + R - 1 <= plast; p += R) {
         step(std::integral_constant<int, 0>{}, p);
         step(std::integral_constant<int, 1>{}, p + 1);
@@ -264,16 +281,17 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, int R>
+template <typename T, int V, int RY, int NW, int K, int R, bool XD = true>
 int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
     using Tl = BKTile<T, V, RY, NW, K>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
-    if (g.plane >= (int64_t(1) << 31)) return set_error(STENCIL_EINVAL, "plane too large for boxk (2^31 elements)");
+    if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 4 * K >= (int64_t(1) << 30))
+        return set_error(STENCIL_EINVAL, "plane too large for boxk (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = boxk_27pt<T, V, RY, NW, K, R>;
+    auto kern = boxk_27pt<T, V, RY, NW, K, R, XD>;
     int zc = env_int("STENCIL_BOXK_ZCHUNK", 0);
     if (zc <= 0) {
         // as kernels_temporalk.hip, with the 3K-plane pipeline fill of this kernel
@@ -324,7 +342,15 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 408: return launch_bk<float, 4, 4, 8, 2, 2>(l, in, out, begin, end, s);
             case 208: return launch_bk<float, 4, 2, 8, 2, 2>(l, in, out, begin, end, s);
             case 116: return launch_bk<float, 4, 1, 16, 2, 2>(l, in, out, begin, end, s);
-            default: return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            case 1116: return launch_bk<float, 2, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
+            case 1416: return launch_bk<float, 4, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
+            case 1216: return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            default:
+                // measured (tools/box_ab.sh): 16-B lanes with LDS x-neighbours
+                // on wide rows (2048^2 x 256: 735 vs 685 Gcell/s), 8-B lanes
+                // with DPP on narrow ones (512^3: 582 vs 504)
+                if (l.prob.nx >= 1024) return launch_bk<float, 4, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
+                return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
             }
         }
         if (steps == 3) {
@@ -341,6 +367,7 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 408: return launch_bk<double, 2, 4, 8, 2, 2>(l, in, out, begin, end, s);
             case 212: return launch_bk<double, 2, 2, 12, 2, 2>(l, in, out, begin, end, s);
             case 208: return launch_bk<double, 2, 2, 8, 2, 2>(l, in, out, begin, end, s);
+            case 1116: return launch_bk<double, 2, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
             default: return launch_bk<double, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
             }
         }

@@ -173,7 +173,7 @@ def test_tkstrip_chunking(gpu, monkeypatch, steps, strip, zchunk, dtype, shape3)
         assert same_bits(got, want), it
 
 
-@pytest.mark.parametrize("cfg", ["default", "308", "216"])
+@pytest.mark.parametrize("cfg", ["default", "308", "216", "1116", "208", "116", "1416", "1216"])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 def test_boxk_chunking(gpu, monkeypatch, cfg, zchunk, dtype):
