@@ -50,15 +50,14 @@ __device__ __forceinline__ T cell2d(const T* c, int row, T avg) {
     }
 }
 
-constexpr int kWaves = 4;
 constexpr int kRX = 64;  // region width: one column per lane
-constexpr int kRY = 32;  // region height: kRY / kWaves rows per wave
+// region height kRY = NW * rows per wave; NW waves (template parameters)
 
 // LDS image of the region with an R-cell pad on every side, so every
 // neighbour read of every lane is in bounds: the sweep is computed for all
 // rows unconditionally (all LDS reads of a step can be in flight together)
 // and only the stores are predicated.
-template <typename T, int ORDER, int R>
+template <typename T, int ORDER, int R, int kWaves, int kRY>
 __global__ void __launch_bounds__(64 * kWaves)
     tb2d(const T* __restrict__ in, T* __restrict__ out, Geom g, int steps, int tiles_x, T avg) {
     constexpr int LXS = kRX + 2 * R + 1;  // odd stride: a column spreads over banks
@@ -130,8 +129,10 @@ __global__ void __launch_bounds__(64 * kWaves)
     }
 }
 
-template <typename T, int ORDER, int R>
+template <typename T, int ORDER, int R, int kWaves, int kRY>
 int launch_tb(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
+    static_assert(kRY % kWaves == 0, "rows per wave");
+    static_assert(size_t(2) * (kRY + 2 * R) * (kRX + 2 * R + 1) * sizeof(T) <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     if (g.nx <= 0 || g.ny <= 0 || steps <= 0) return STENCIL_OK;
     const int ring = steps * R;
@@ -139,19 +140,38 @@ int launch_tb(const stencil_layout& l, const void* in, void* out, int steps, hip
     if (TX < 4 || TY < 4) return set_error(STENCIL_EINVAL, "tb2d: %d steps of radius %d leave no tile", steps, R);
     const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
     if (tx * ty > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "tb2d: grid too large");
-    hipLaunchKernelGGL((tb2d<T, ORDER, R>), dim3(unsigned(tx * ty)), dim3(64, kWaves), 0, s,
+    hipLaunchKernelGGL((tb2d<T, ORDER, R, kWaves, kRY>), dim3(unsigned(tx * ty)), dim3(64, kWaves), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, steps, int(tx), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
 
+int tenv_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+}
+
+// region shapes (STENCIL_TB2D_CFG = waves * 1000 + region height)
+template <typename T, int ORDER, int R>
+int launch_shape(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
+    // default 64 x 64 regions, 8 waves (1024^2, K = 8: fp64 400 vs 312
+    // Gcell/s for 64 x 32 / 4 waves, fp32 520 vs 460; tools/tb2d_ab.sh)
+    switch (tenv_int("STENCIL_TB2D_CFG", 0)) {
+    case 4032: return launch_tb<T, ORDER, R, 4, 32>(l, in, out, steps, s);
+    case 16128: return launch_tb<T, ORDER, R, 16, 128>(l, in, out, steps, s);
+    case 12096: return launch_tb<T, ORDER, R, 12, 96>(l, in, out, steps, s);
+    case 8128: return launch_tb<T, ORDER, R, 8, 128>(l, in, out, steps, s);
+    default: return launch_tb<T, ORDER, R, 8, 64>(l, in, out, steps, s);
+    }
+}
+
 template <typename T, int ORDER>
 int launch_r(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
     switch (l.prob.radius) {
-    case 1: return launch_tb<T, ORDER, 1>(l, in, out, steps, s);
-    case 2: return launch_tb<T, ORDER, 2>(l, in, out, steps, s);
-    case 3: return launch_tb<T, ORDER, 3>(l, in, out, steps, s);
-    case 4: return launch_tb<T, ORDER, 4>(l, in, out, steps, s);
+    case 1: return launch_shape<T, ORDER, 1>(l, in, out, steps, s);
+    case 2: return launch_shape<T, ORDER, 2>(l, in, out, steps, s);
+    case 3: return launch_shape<T, ORDER, 3>(l, in, out, steps, s);
+    case 4: return launch_shape<T, ORDER, 4>(l, in, out, steps, s);
     default: return set_error(STENCIL_EUNSUPPORTED, "tb2d: radius > 4");
     }
 }
@@ -164,9 +184,11 @@ bool tb2d_supports(const stencil_problem& p) {
 
 int tb2d_max_steps(const stencil_problem& p) {
     const char* e = std::getenv("STENCIL_TB2D_K");
-    int k = e && *e ? std::atoi(e) : 8;
-    // keep the output tile at least half the 32-row region
-    const int cap = std::max(1, 8 / p.radius);
+    const bool forced = e && *e;
+    const int k = forced ? std::atoi(e) : 8;
+    // default: keep the output tile at least half of a 32-row region; an
+    // explicit K may go up to a 16-cell-wide tile of the 64-wide region
+    const int cap = std::max(1, (forced ? 24 : 8) / p.radius);
     return std::max(1, std::min(k, cap));
 }
 

@@ -77,13 +77,19 @@ def test_2d_radius_random(gpu, r, order):
     assert same_bits(got, want)
 
 
-@pytest.mark.parametrize("k", ["1", "3", "8"])
+@pytest.mark.parametrize("k", ["1", "3", "8", "12"])
 @pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma"), (3, "dma"), (4, "naive")])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype):
-    """kernels_tb2d.hip: K sweeps per launch in LDS, ragged grids spanning
-    several tiles, iteration counts that leave a partial last launch."""
+@pytest.mark.parametrize("cfg", ["default", "4032", "16128", "12096", "8128"])
+def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
+    """kernels_tb2d.hip: K sweeps per launch in LDS, every region shape,
+    ragged grids spanning several tiles, iteration counts that leave a partial
+    last launch."""
     monkeypatch.setenv("STENCIL_TB2D_K", k)
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_TB2D_CFG", cfg)
+    if int(k) * r > 12 and cfg == "4032":
+        pytest.skip("tile of the 32-row region would be empty")
     for nx, ny, it in ((301, 170, 11), (5, 3, 4), (64, 200, 9)):
         p = ob.problem(2, dtype, "star", r, order, nx, ny)
         want = ob.run(p, it, "random", 8 + r)

@@ -39,7 +39,11 @@ def main():
     shape = [int(v) for v in os.environ.get("TUNE_SHAPE", f"{n},{n},{n}").split(",")]
     stencil = os.environ.get("TUNE_STENCIL", "star")
     sweepk = int(os.environ.get("TUNE_SWEEPK", "0"))
-    eng = JacobiEngine(StencilSpec(dims=3, dtype=dtype, kernel=kernel, shape=stencil), *shape)
+    dims = int(os.environ.get("TUNE_DIMS", "3"))
+    order = os.environ.get("TUNE_ORDER", "naive")
+    if dims == 2:
+        shape = shape[:2] + [1]
+    eng = JacobiEngine(StencilSpec(dims=dims, dtype=dtype, kernel=kernel, shape=stencil, order=order), *shape)
     cells = shape[0] * shape[1] * shape[2]
     eng.reset()
     es = 8 if dtype == "fp64" else 4
