@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: 3D 7-point fp64 Jacobi (BASELINE.json metric, config 2 size per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+--config picks another BASELINE.json config as the workload (C3: 4096^3 fp32,
+C4: 2048x2048x4096 fp64, C5: 2048^3 27-point fp64), its global grid z-slab
+split over the N ranks; the default C2 is the metric's own config.
 
 One step = one Jacobi sweep of the whole grid.  At N=1 the workload is
 BASELINE config 2 (512^3 interior, fp64, 7-point star; the default K=1000 is
@@ -33,9 +37,27 @@ METRIC = "Gcell-updates/s + achieved HBM GB/s vs roofline, 7-pt fp64 Jacobi, 1/2
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
 
 
+# BASELINE.json configs as bench workloads.  C2 (the default, the metric's
+# config) is weak-scaled: n^3 per GPU.  C3-C5 are the configs' global grids,
+# z-slab split over the ranks (strong scaling); they need as many GPUs as
+# their two grids need memory (C3: 2 x 275 GB, C4: 2 x 137 GB).
+PRESETS = {
+    "C2": dict(dtype="fp64", shape="star", grid=None, min_gpus=1,
+               desc="BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU"),
+    "C3": dict(dtype="fp32", shape="star", grid=(4096, 4096, 4096), min_gpus=2,
+               desc="BASELINE config 3: 3D 7-point fp32 Jacobi, 4096^3"),
+    "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=2,
+               desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
+    "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
+               desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, 2-step temporal blocking"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="C2", choices=sorted(PRESETS),
+                    help="workload (default C2, the metric's config; C3-C5 split a global grid over the ranks)")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
@@ -61,20 +83,22 @@ def host_threads() -> int:
     return max(1, min(n, int(env))) if env.isdigit() and int(env) > 0 else n
 
 
-def cpu_baseline(n: int, budget_s: float, threads: int = 1):
+def cpu_baseline(n: int, budget_s: float, threads: int = 1, dtype: str = "fp64", shape: str = "star"):
     """The oracle (port of check_result's loop, stencil.cpp:94-131, generalised
-    to 3D) on the host over a bounded number of sweeps of the same 512^3 fp64
-    grid: single-threaded like the reference's own CPU path, or with OpenMP
-    over `threads` cores (identical per-cell arithmetic, bitwise-equal result)."""
+    to 3D) on the host over a bounded number of sweeps of an n^3 grid of the
+    workload's stencil: single-threaded like the reference's own CPU path, or
+    with OpenMP over `threads` cores (identical per-cell arithmetic,
+    bitwise-equal result)."""
     from oracle import binding as ob
-    p = ob.problem(3, "fp64", "star", 1, "naive", n, n, n)
+    p = ob.problem(3, dtype, shape, 1, "naive", n, n, n)
     t1 = ob.timed_run(p, 1, threads=threads)
     iters = max(1, min(200, int(budget_s / max(t1, 1e-6))))
     t = ob.timed_run(p, iters, threads=threads)
     cells = float(n) ** 3 * iters
     who = "1 host thread" if threads == 1 else f"{threads} host threads (OpenMP)"
+    pts = "7-point" if shape == "star" else "27-point"
     return {"value": round(cells / t / 1e9, 4), "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ naive sweep, {n}^3 fp64 7-point, {iters} sweeps from the reference initial "
+            "sample": f"oracle/ naive sweep, {n}^3 {dtype} {pts}, {iters} sweeps from the reference initial "
                       f"condition, {t:.1f} s on {who}"}
 
 
@@ -95,7 +119,7 @@ def main():
 
     from stencil_amd import _lib
     from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
-    from stencil_amd.slab import HostStagedExchanger, SlabInfo, SlabJacobi, TorchDistExchanger
+    from stencil_amd.slab import HostStagedExchanger, SlabInfo, SlabJacobi, TorchDistExchanger, partition
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -113,18 +137,27 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    pre = PRESETS[args.config]
+    if world < pre["min_gpus"]:
+        raise SystemExit(f"--config {args.config} needs at least {pre['min_gpus']} GPUs (grid memory)")
     n = args.n
+    if pre["grid"] is None:  # weak scaling: n^3 per rank
+        gnx, gny, gnz = n, n, n * world
+        first, count = rank * n, n
+    else:                    # strong scaling: the global grid split in z-slabs
+        gnx, gny, gnz = pre["grid"]
+        first, count = partition(gnz, world, rank)
     # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
-    # 4 for the 7-point star) so K sweeps fuse across the exchange too (one
-    # K-plane exchange per K-sweep round).
-    spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=1, order="naive", kernel=args.kernel)
-    fuse = JacobiEngine(spec, n, n, n, device=local, allocate=False).fuse_steps
+    # 4 for the 7-point star, 2 for the box) so K sweeps fuse across the
+    # exchange too (one K-plane exchange per K-sweep round).
+    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
+    fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps
     if world > 1:
         spec = dataclasses.replace(spec, halo=max(2, fuse))
     flags = (_lib.HALO_LO if rank > 0 else 0) | (_lib.HALO_HI if rank < world - 1 else 0)
-    eng = JacobiEngine(spec, n, n, n, device=local, flags=flags)
+    eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
     exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
-    slab = SlabJacobi(eng, SlabInfo(rank, world, rank * n, n), exchanger, overlap=not args.no_overlap)
+    slab = SlabJacobi(eng, SlabInfo(rank, world, first, count), exchanger, overlap=not args.no_overlap)
     slab.init("reference")
     kernel_id = eng.plan(12)[1]
     kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
@@ -161,13 +194,13 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
 
-    cells_per_gpu = float(n) ** 3
-    total_updates = cells_per_gpu * world * args.steps
+    cells_per_gpu = float(gnx) * gny * count  # this rank's; rank 0 owns the largest slab
+    total_updates = float(gnx) * gny * gnz * args.steps
     gcell = total_updates / elapsed / 1e9
-    bytes_per_update = 2 * 8
+    bytes_per_update = 2 * spec.elem_bytes
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
     edge = slab.depth if slab.fused else max(1, slab.depth)
-    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (n - 2 * edge) / n
+    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (count - 2 * edge) / count
     alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
     if world == 1:
         # device time per `sweeps_per_launch` sweeps, charged pro rata (with
@@ -179,7 +212,8 @@ def main():
     achieved = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
 
     if rank == 0:
-        workload = f"3d7pt_fp64_{n}cube_per_gpu"
+        workload = f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{count}"
+        desc = pre["desc"].format(n=n)
         out = {
             "metric": METRIC,
             "value": round(gcell, 3),
@@ -189,14 +223,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if pre["grid"] is None else "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if spec.dtype == "fp64" else "f32",
             "data": "synthetic: the reference initial condition (x-ghost faces 1, everything else 0)",
             "config": {
-                "workload": f"BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU "
-                            f"(global {n}x{n}x{n * world}), one step = one sweep",
-                "grid": [n, n, n * world],
+                "workload": f"{desc} (global {gnx}x{gny}x{gnz}), one step = one sweep",
+                "grid": [gnx, gny, gnz],
                 "kernel": kname,
                 "parallelism": f"z-slab x{world}" + ("" if world == 1 else
                                                      ", RCCL halo P2P overlapped" if args.exchange == "nccl"
@@ -221,9 +254,11 @@ def main():
         except Exception as exc:  # calibration only
             out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+            cb = dict(dtype=spec.dtype, shape=spec.shape)
+            out["cpu_baseline"] = cpu_baseline(min(n, 512), args.cpu_seconds, **cb)
             # the same loop with OpenMP over the host's cores too
-            out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads())
+            out["cpu_baseline_all_cores"] = cpu_baseline(min(n, 512), args.cpu_seconds / 2,
+                                                         threads=host_threads(), **cb)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
