@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host"],
+    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback"],
                     help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank uses GPU 0 (needs --exchange host)")
@@ -119,13 +119,17 @@ def main():
 
     from stencil_amd import _lib
     from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
-    from stencil_amd.slab import HostStagedExchanger, SlabInfo, SlabJacobi, TorchDistExchanger, partition
+    from stencil_amd.slab import (HostStagedExchanger, LoopbackExchanger, SlabInfo, SlabJacobi, TorchDistExchanger,
+                                  partition)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    loop = args.exchange == "loopback"  # 1 process, 1 GPU, the structure of an interior rank
+    if loop and world != 1:
+        raise SystemExit("--exchange loopback is a single-process rehearsal")
     if args.share_device:
         if args.exchange != "host":
             raise SystemExit("--share-device needs --exchange host (RCCL refuses two ranks on one GPU)")
@@ -152,16 +156,22 @@ def main():
     # exchange too (one K-plane exchange per K-sweep round).
     spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
     fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps
-    if world > 1:
+    if world > 1 or loop:
         spec = dataclasses.replace(spec, halo=max(2, fuse))
-    flags = (_lib.HALO_LO if rank > 0 else 0) | (_lib.HALO_HI if rank < world - 1 else 0)
+    flags = (_lib.HALO_LO if rank > 0 or loop else 0) | (_lib.HALO_HI if rank < world - 1 or loop else 0)
     eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
-    exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
-    slab = SlabJacobi(eng, SlabInfo(rank, world, first, count), exchanger, overlap=not args.no_overlap)
+    if loop:
+        exchanger = LoopbackExchanger()
+        info = SlabInfo(0, 3, first, count)  # drives the multi-rank round structure
+    else:
+        exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
+        info = SlabInfo(rank, world, first, count)
+    slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
     slab.init("reference")
     kernel_id = eng.plan(12)[1]
     kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
-    sweeps_per_launch = eng.fuse_steps if world == 1 else slab.launches_per_round()
+    multi = world > 1 or loop  # the slab round structure (exchange + two streams)
+    sweeps_per_launch = eng.fuse_steps if not multi else slab.launches_per_round()
 
     def barrier():
         if world > 1:
@@ -169,7 +179,7 @@ def main():
         torch.cuda.synchronize()
 
     # ---------------- warmup
-    if world == 1:
+    if not multi:
         eng.iterate(args.warmup)
     else:
         slab.run(args.warmup)
@@ -178,7 +188,7 @@ def main():
     # ---------------- timed region: exactly K sweeps
     stream = torch.cuda.current_stream()
     t0 = time.perf_counter()
-    if world == 1:
+    if not multi:
         _, dev_ms = eng.iterate(args.steps, stream=stream, timed=True)
         kernel_ms_total = dev_ms
         kernel_launches = eng.plan(args.steps)[0]
@@ -200,9 +210,9 @@ def main():
     bytes_per_update = 2 * spec.elem_bytes
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
     edge = slab.depth if slab.fused else max(1, slab.depth)
-    cells_per_launch = cells_per_gpu if world == 1 else cells_per_gpu * (count - 2 * edge) / count
+    cells_per_launch = cells_per_gpu if not multi else cells_per_gpu * (count - 2 * edge) / count
     alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
-    if world == 1:
+    if not multi:
         # device time per `sweeps_per_launch` sweeps, charged pro rata (with
         # K = 4 a 1000-step job is 250 fused launches; a K that does not divide
         # the step count adds a remainder pair / single sweep)
@@ -231,7 +241,9 @@ def main():
                 "workload": f"{desc} (global {gnx}x{gny}x{gnz}), one step = one sweep",
                 "grid": [gnx, gny, gnz],
                 "kernel": kname,
-                "parallelism": f"z-slab x{world}" + ("" if world == 1 else
+                "parallelism": (f"z-slab x{world}" if not loop else
+                                "1 GPU rehearsing an interior rank (periodic loopback halo, two streams)") +
+                               ("" if not multi or loop else
                                                      ", RCCL halo P2P overlapped" if args.exchange == "nccl"
                                                      else ", host-staged gloo halo (rehearsal)"),
                 "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
@@ -253,7 +265,7 @@ def main():
             out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
         except Exception as exc:  # calibration only
             out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not loop and not args.no_cpu_baseline:
             cb = dict(dtype=spec.dtype, shape=spec.shape)
             out["cpu_baseline"] = cpu_baseline(min(n, 512), args.cpu_seconds, **cb)
             # the same loop with OpenMP over the host's cores too

@@ -84,6 +84,22 @@ class HostStagedExchanger(TorchDistExchanger):
         return []
 
 
+class LoopbackExchanger:
+    """Rehearsal on ONE GPU of a rank with two neighbours: the slab's own
+    boundary planes become its halos (periodic in z), copied device to device
+    on the calling stream.  The numbers change (periodic instead of
+    Dirichlet z faces); the per-round launch and stream structure of an
+    interior rank does not (bench.py --exchange loopback)."""
+
+    def __init__(self, rank: int = 0, world: int = 1):
+        self.rank, self.world = rank, world
+
+    def exchange(self, send_lo, send_hi, recv_lo, recv_hi):
+        recv_lo.copy_(send_hi, non_blocking=True)
+        recv_hi.copy_(send_lo, non_blocking=True)
+        return []
+
+
 @dataclass
 class SlabInfo:
     rank: int
@@ -111,6 +127,7 @@ class SlabJacobi:
         self.cur, self.nxt = backend.a, backend.b
         self.on_gpu = self.cur.device.type == "cuda"
         self._timing = None  # list of (start, end) events around interior sweeps
+        self._ev_bnd = self._ev_int = None  # last round's boundary / interior completion
         if self.on_gpu:
             self.stream_bnd = torch.cuda.Stream(device=self.cur.device, priority=-1)  # high priority
             self.stream_int = torch.cuda.Stream(device=self.cur.device)
@@ -161,14 +178,27 @@ class SlabJacobi:
             for w in works:
                 w.wait()
         else:
-            main = torch.cuda.current_stream()
+            # Rounds chain on the two streams directly, not through the
+            # caller's stream (each cross-queue hop costs ~15 us on MI355X:
+            # a main-stream join per round measured 30 us of idle GPU between
+            # rounds).  Dependencies of round r (src = dst of round r-1):
+            #   interior(r) reads src [0, n): after boundary(r-1)   (sa event)
+            #   boundary(r) reads src incl. the halos received by exchange(r-1)
+            #     (on sa already) and planes interior(r-1) wrote, and
+            #     overwrites planes interior(r-1) read: after interior(r-1)
+            #   exchange(r) after boundary(r) (same stream); the P2P's
+            #   completion is waited for on sa, ahead of boundary(r+1).
+            # finish() joins both streams into the caller's stream.
             sa, sb = self.stream_bnd, self.stream_int
-            sa.wait_stream(main)
-            sb.wait_stream(main)
-            with torch.cuda.stream(sa):
-                update(src, dst, 0, edge, sa)
-                update(src, dst, n - edge, n, sa)
-                works = self.ex.exchange(*self._halo_views(dst))
+            if self._ev_bnd is None:
+                main = torch.cuda.current_stream()
+                sa.wait_stream(main)
+                sb.wait_stream(main)
+            else:
+                sb.wait_event(self._ev_bnd)
+                sa.wait_event(self._ev_int)
+            # The interior launch is enqueued first: one workgroup per CU, it
+            # takes the CUs it needs and the boundary launches run on the rest.
             with torch.cuda.stream(sb):
                 if self._timing is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
@@ -178,23 +208,48 @@ class SlabJacobi:
                 if self._timing is not None:
                     ev1.record(sb)
                     self._timing.append((ev0, ev1))
-            for w in works:
-                w.wait()  # current (main) stream waits for the P2P
-            main.wait_stream(sa)
-            main.wait_stream(sb)
+                self._ev_int = torch.cuda.Event()
+                self._ev_int.record(sb)
+            with torch.cuda.stream(sa):
+                update(src, dst, 0, edge, sa)
+                update(src, dst, n - edge, n, sa)
+                self._ev_bnd = torch.cuda.Event()
+                self._ev_bnd.record(sa)
+                for w in self.ex.exchange(*self._halo_views(dst)):
+                    w.wait()  # sa waits for the P2P
         self.cur, self.nxt = dst, src
+
+    def finish(self) -> None:
+        """Join the round streams into the caller's stream (after run())."""
+        if self.on_gpu and self._ev_bnd is not None:
+            main = torch.cuda.current_stream()
+            main.wait_stream(self.stream_bnd)
+            main.wait_stream(self.stream_int)
+        self._ev_bnd = self._ev_int = None
+
+    def _step(self) -> None:
+        self._round(lambda s, d, b, e, st: self.be.sweep(s, d, b, e, stream=st), max(self.r, self.depth))
+
+    def _step2(self) -> None:
+        self._round(lambda s, d, b, e, st: self.be.sweep2(s, d, b, e, stream=st), self.depth)
+
+    def _stepk(self, k: int) -> None:
+        self._round(lambda s, d, b, e, st: self.be.sweepk(s, d, b, e, k, stream=st), self.depth)
 
     def step(self) -> None:
         """One sweep."""
-        self._round(lambda s, d, b, e, st: self.be.sweep(s, d, b, e, stream=st), max(self.r, self.depth))
+        self._step()
+        self.finish()
 
     def step2(self) -> None:
         """Two sweeps, fused (needs backend.fused and halo depth >= 2)."""
-        self._round(lambda s, d, b, e, st: self.be.sweep2(s, d, b, e, stream=st), self.depth)
+        self._step2()
+        self.finish()
 
     def stepk(self, k: int) -> None:
         """k sweeps fused in one launch per plane range (halo depth >= k)."""
-        self._round(lambda s, d, b, e, st: self.be.sweepk(s, d, b, e, k, stream=st), self.depth)
+        self._stepk(k)
+        self.finish()
 
     def step2_split(self) -> None:
         """Two single sweeps per exchange of 2 planes (halo depth >= 2): the
@@ -202,6 +257,7 @@ class SlabJacobi:
         second the owned planes -- communication-avoiding temporal blocking
         with the single-sweep kernel (used where no fused kernel is faster).
         The result lands back in the current grid."""
+        self.finish()  # this round joins through the caller's stream
         src, dst = self.cur, self.nxt
         n, be, sl = self.slab.count, self.be, self.slab
         lo = -1 if sl.rank > 0 else 0
@@ -277,21 +333,22 @@ class SlabJacobi:
         if mode == "fused":
             k = self.k
             for _ in range(iterations // k):
-                self.stepk(k) if k != 2 else self.step2()
+                self._stepk(k) if k != 2 else self._step2()
             rem = iterations % k
             if rem >= 2:
-                self.step2()
+                self._step2()
                 rem -= 2
             if rem:
-                self.step()
+                self._step()
         elif mode == "split2":
             for _ in range(iterations // 2):
                 self.step2_split()
             if iterations % 2:
-                self.step()
+                self._step()
         else:
             for _ in range(iterations):
-                self.step()
+                self._step()
+        self.finish()
 
     def launches_per_round(self) -> int:
         """Sweeps per timed interior launch (the bench's roofline unit)."""
