@@ -11,10 +11,13 @@ with rank-1 and rank+1 -- no packing, and on an 8-GPU MI355X node every
 neighbour pair has its own xGMI link.
 
 Per round, on each rank (overlap=True):
-  stream A: update the boundary planes -> post send/recv of them to the
-            neighbours (torch.distributed P2P; RCCL on GPUs, gloo on CPUs);
+  stream A: update the boundary planes (high priority) -> post send/recv of
+            them to the neighbours (torch.distributed P2P; RCCL on GPUs, gloo
+            on CPUs);
   stream B: update the interior planes meanwhile;
-  join:     the next round waits for both streams and the received halos.
+  chain:    round r+1's interior waits for round r's boundary launches, its
+            boundary launches for round r's interior and the received halos
+            (events between the two streams; see _round).
 A round is one sweep (halo depth r), or -- when the backend has a fused
 multi-step kernel and K-deep halos -- K sweeps in one launch per plane range
 (temporal blocking across GPUs: the exchange of K planes every K sweeps, the
@@ -129,7 +132,14 @@ class SlabJacobi:
         self._timing = None  # list of (start, end) events around interior sweeps
         self._ev_bnd = self._ev_int = None  # last round's boundary / interior completion
         if self.on_gpu:
-            self.stream_bnd = torch.cuda.Stream(device=self.cur.device, priority=-1)  # high priority
+            # The boundary stream has the high priority, so the boundary
+            # planes and their exchange come first and stay off the critical
+            # path.  Traced on one GPU (bench.py --exchange loopback): with
+            # the interior first, the boundary launches only get the CUs the
+            # interior leaves free and share HBM with it, and take ~480 us of
+            # a ~500 us round -- an RCCL exchange behind them would then set
+            # the round time; boundary first costs the interior ~25 us.
+            self.stream_bnd = torch.cuda.Stream(device=self.cur.device, priority=-1)
             self.stream_int = torch.cuda.Stream(device=self.cur.device)
 
     # -------------------------------------------------------------- helpers
@@ -197,8 +207,6 @@ class SlabJacobi:
             else:
                 sb.wait_event(self._ev_bnd)
                 sa.wait_event(self._ev_int)
-            # The interior launch is enqueued first: one workgroup per CU, it
-            # takes the CUs it needs and the boundary launches run on the rest.
             with torch.cuda.stream(sb):
                 if self._timing is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
