@@ -146,6 +146,168 @@ int launch_tb(const stencil_layout& l, const void* in, void* out, int steps, hip
     return STENCIL_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Strip variant (R <= V): each wave keeps RY consecutive rows of the region in
+// registers (V cells per lane), x-neighbours come from the lane's own cells
+// and DPP lane shifts, y-neighbours from its own rows; only the R top and R
+// bottom rows of each wave's strip go through LDS (double-buffered by sweep
+// parity: one barrier per sweep).  The LDS sweep of tb2d reads 4 LDS values
+// per cell (measured 1.5 us per sweep on a 64 x 64 region); here a wave
+// moves 2R rows through LDS per sweep.  Same arithmetic order as cell2d.
+template <typename T, int V>
+struct Vec2 {
+    typedef T type __attribute__((ext_vector_type(V)));
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp2(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp2(double v) {
+    const int2 b = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_mov_dpp(b.x, CTRL, 0xf, 0xf, true),
+                                                 __builtin_amdgcn_mov_dpp(b.y, CTRL, 0xf, 0xf, true)));
+}
+
+template <typename T, int ORDER, int R, int V, int RY, int NW>
+__global__ void __launch_bounds__(64 * NW)
+    tb2ds(const T* __restrict__ in, T* __restrict__ out, Geom g, int steps, int tiles_x, T avg) {
+    static_assert(R <= V, "one DPP shift reaches R cells");
+    static_assert(RY >= R, "a strip holds at least R rows");
+    using VT = typename Vec2<T, V>::type;
+    constexpr int RW = 64 * V, RH = NW * RY;
+    __shared__ __attribute__((aligned(16))) T L[2][NW][2][R][RW];  // [parity][wave][top, bottom][row][x]
+    const int H = steps * R;
+    const int TX = RW - 2 * H, TY = RH - 2 * H;
+    const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x = int64_t(bx) * TX - H + int64_t(lane) * V;
+    const int64_t yw = int64_t(by) * TY - H + int64_t(w) * RY;
+    const T* __restrict__ src = in + g.origin;
+    T* __restrict__ dst = out + g.origin;
+
+    bool xin[V], xld[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        xin[j] = x + j >= 0 && x + j < g.nx;
+        xld[j] = x + j >= -R && x + j < g.nx + R;
+    }
+    bool yin[RY];
+    VT c0[RY], c1[RY];
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int64_t y = yw + k;
+        yin[k] = y >= 0 && y < g.ny;
+        const bool yld = y >= -R && y < g.ny + R;
+#pragma unroll
+        for (int j = 0; j < V; ++j) c0[k][j] = (yld && xld[j]) ? src[y * g.row + x + j] : T(0);
+        c1[k] = c0[k];
+    }
+    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+    const int xl = lane * V;
+
+    // one sweep a -> b, boundary rows through LDS buffer P
+    auto sweep = [&](const VT (&a)[RY], VT (&b)[RY], int P) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            *reinterpret_cast<VT*>(&L[P][w][0][i][xl]) = a[i];
+            *reinterpret_cast<VT*>(&L[P][w][1][i][xl]) = a[RY - R + i];
+        }
+        __syncthreads();
+        VT above[R], below[R];  // rows -R..-1 and RY..RY+R-1 of this strip
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            above[i] = *reinterpret_cast<const VT*>(&L[P][wa][1][i][xl]);
+            below[i] = *reinterpret_cast<const VT*>(&L[P][wb][0][i][xl]);
+        }
+#pragma unroll
+        for (int k = 0; k < RY; ++k) {
+            auto rowv = [&](int m) -> VT {  // strip row m in [-R, RY+R)
+                if (m < 0) return above[m + R];
+                if (m >= RY) return below[m - RY];
+                return a[m];
+            };
+            const VT cv = a[k];
+            // x-neighbour cells of this lane's V cells: [-R, V+R)
+            T xs[V + 2 * R];
+#pragma unroll
+            for (int j = 0; j < V; ++j) xs[R + j] = cv[j];
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                xs[i] = dpp2<0x138>(cv[V - R + i]);   // wave_shr:1: lane-1's cells
+                xs[R + V + i] = dpp2<0x130>(cv[i]);   // wave_shl:1: lane+1's cells
+            }
+            VT o;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                T r;
+                if constexpr (ORDER == STENCIL_ORDER_DMA && R == 1) {
+                    r = T(0.25) * (((rowv(k - 1)[j] + xs[R + j - 1]) + xs[R + j + 1]) + rowv(k + 1)[j]);
+                } else if constexpr (ORDER == STENCIL_ORDER_DMA) {
+                    T sum = T(0);
+#pragma unroll
+                    for (int d = -R; d <= R; ++d) sum += xs[R + j + d];
+#pragma unroll
+                    for (int d = -R; d <= R; ++d) sum += rowv(k + d)[j];
+                    sum -= cv[j] + cv[j];
+                    r = sum * avg;
+                } else {
+                    T sum = T(0);
+#pragma unroll
+                    for (int d = R; d >= 1; --d) sum += xs[R + j - d];
+#pragma unroll
+                    for (int d = 1; d <= R; ++d) sum += xs[R + j + d];
+#pragma unroll
+                    for (int d = R; d >= 1; --d) sum += rowv(k - d)[j];
+#pragma unroll
+                    for (int d = 1; d <= R; ++d) sum += rowv(k + d)[j];
+                    r = sum * avg;
+                }
+                o[j] = (xin[j] && yin[k]) ? r : cv[j];  // ghost cells keep their value
+            }
+            b[k] = o;
+        }
+    };
+    int s = 0;
+    for (; s + 2 <= steps; s += 2) {
+        sweep(c0, c1, 0);
+        sweep(c1, c0, 1);
+    }
+    if (s < steps) {
+        sweep(c0, c1, 0);
+#pragma unroll
+        for (int k = 0; k < RY; ++k) c0[k] = c1[k];
+    }
+    // the tile: region columns [H, H + TX), rows [H, H + TY)
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int rr = w * RY + k;
+        const int64_t y = yw + k;
+        if (rr < H || rr >= H + TY || y >= g.ny) continue;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int cx = xl + j;
+            if (cx >= H && cx < H + TX && x + j < g.nx) dst[y * g.row + x + j] = c0[k][j];
+        }
+    }
+}
+
+template <typename T, int ORDER, int R, int V, int RY, int NW>
+int launch_tbs(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
+    const Geom g = geom_of(l);
+    if (g.nx <= 0 || g.ny <= 0 || steps <= 0) return STENCIL_OK;
+    const int ring = steps * R;
+    const int TX = 64 * V - 2 * ring, TY = NW * RY - 2 * ring;
+    if (TX < 4 || TY < 4) return set_error(STENCIL_EINVAL, "tb2ds: %d steps of radius %d leave no tile", steps, R);
+    const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
+    if (tx * ty > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "tb2ds: grid too large");
+    hipLaunchKernelGGL((tb2ds<T, ORDER, R, V, RY, NW>), dim3(unsigned(tx * ty)), dim3(64, NW), 0, s,
+                       static_cast<const T*>(in), static_cast<T*>(out), g, steps, int(tx), avg_weight<T>(l.prob));
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
 int tenv_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e && *e ? std::atoi(e) : dflt;
@@ -154,10 +316,28 @@ int tenv_int(const char* name, int dflt) {
 // region shapes (STENCIL_TB2D_CFG = waves * 1000 + region height)
 template <typename T, int ORDER, int R>
 int launch_shape(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
+    const int cfg = tenv_int("STENCIL_TB2D_CFG", 0);
+    if constexpr (R <= 2) {
+        // strip variants: 9 V RY NW (V cells per lane, RY rows per wave, NW waves)
+        switch (cfg) {
+        case 92808: return launch_tbs<T, ORDER, R, 2, 8, 8>(l, in, out, steps, s);
+        case 92816: return launch_tbs<T, ORDER, R, 2, 8, 16>(l, in, out, steps, s);
+        case 92408: return launch_tbs<T, ORDER, R, 2, 4, 8>(l, in, out, steps, s);
+        case 94808: return launch_tbs<T, ORDER, R, 4, 8, 8>(l, in, out, steps, s);
+        case 92608: return launch_tbs<T, ORDER, R, 2, 6, 8>(l, in, out, steps, s);
+        case 0:
+            // default for r <= 2: 128 x 64 regions (2 cells per lane, 8 rows x 8
+            // waves); 1024^2, K = 8: fp64 559 vs 393 Gcell/s for the LDS kernel,
+            // fp32 709 vs 520 (tools/tb2d_ab.sh)
+            return launch_tbs<T, ORDER, R, 2, 8, 8>(l, in, out, steps, s);
+        default: break;
+        }
+    }
     // default 64 x 64 regions, 8 waves (1024^2, K = 8: fp64 400 vs 312
     // Gcell/s for 64 x 32 / 4 waves, fp32 520 vs 460; tools/tb2d_ab.sh)
-    switch (tenv_int("STENCIL_TB2D_CFG", 0)) {
+    switch (cfg) {
     case 4032: return launch_tb<T, ORDER, R, 4, 32>(l, in, out, steps, s);
+    case 8064: return launch_tb<T, ORDER, R, 8, 64>(l, in, out, steps, s);
     case 16128: return launch_tb<T, ORDER, R, 16, 128>(l, in, out, steps, s);
     case 12096: return launch_tb<T, ORDER, R, 12, 96>(l, in, out, steps, s);
     case 8128: return launch_tb<T, ORDER, R, 8, 128>(l, in, out, steps, s);

@@ -80,16 +80,21 @@ def test_2d_radius_random(gpu, r, order):
 @pytest.mark.parametrize("k", ["1", "3", "8", "12"])
 @pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma"), (3, "dma"), (4, "naive")])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("cfg", ["default", "4032", "16128", "12096", "8128"])
+@pytest.mark.parametrize("cfg", ["default", "8064", "4032", "16128", "12096", "8128", "92808", "92816", "92408",
+                                 "94808"])
 def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
-    """kernels_tb2d.hip: K sweeps per launch in LDS, every region shape,
-    ragged grids spanning several tiles, iteration counts that leave a partial
-    last launch."""
+    """kernels_tb2d.hip: K sweeps per launch, every region shape of the LDS
+    kernel and of the register-strip kernel (cfg 9xxxx, r <= 2), ragged grids
+    spanning several tiles, iteration counts that leave a partial last launch."""
     monkeypatch.setenv("STENCIL_TB2D_K", k)
     if cfg != "default":
         monkeypatch.setenv("STENCIL_TB2D_CFG", cfg)
-    if int(k) * r > 12 and cfg == "4032":
-        pytest.skip("tile of the 32-row region would be empty")
+    strip = cfg.startswith("9") and r <= 2
+    rw = 64 * int(cfg[1]) if strip else 64
+    rh = {"default": 64, "8064": 64, "4032": 32, "16128": 128, "12096": 96, "8128": 128, "92808": 64, "92816": 128,
+          "92408": 32, "94808": 64}[cfg] if (strip or not cfg.startswith("9")) else 64
+    if min(rw, rh) - 2 * min(int(k), 24 // r) * r < 4:
+        pytest.skip("no tile left in this region for K sweeps")
     for nx, ny, it in ((301, 170, 11), (5, 3, 4), (64, 200, 9)):
         p = ob.problem(2, dtype, "star", r, order, nx, ny)
         want = ob.run(p, it, "random", 8 + r)
