@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback"],
+    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self"],
                     help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank uses GPU 0 (needs --exchange host)")
@@ -119,17 +119,19 @@ def main():
 
     from stencil_amd import _lib
     from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
-    from stencil_amd.slab import (HostStagedExchanger, LoopbackExchanger, SlabInfo, SlabJacobi, TorchDistExchanger,
-                                  partition)
+    from stencil_amd.slab import (HostStagedExchanger, LoopbackExchanger, SelfP2PExchanger, SlabInfo, SlabJacobi,
+                                  TorchDistExchanger, partition)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    loop = args.exchange == "loopback"  # 1 process, 1 GPU, the structure of an interior rank
+    # 1 process, 1 GPU, the structure of an interior rank: halos = own
+    # boundary planes (periodic), by device copies or by RCCL send/recv to self
+    loop = args.exchange in ("loopback", "nccl-self")
     if loop and world != 1:
-        raise SystemExit("--exchange loopback is a single-process rehearsal")
+        raise SystemExit("--exchange loopback / nccl-self are single-process rehearsals")
     if args.share_device:
         if args.exchange != "host":
             raise SystemExit("--share-device needs --exchange host (RCCL refuses two ranks on one GPU)")
@@ -140,6 +142,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    elif args.exchange == "nccl-self":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=0, world_size=1)
 
     pre = PRESETS[args.config]
     if world < pre["min_gpus"]:
@@ -161,7 +167,7 @@ def main():
     flags = (_lib.HALO_LO if rank > 0 or loop else 0) | (_lib.HALO_HI if rank < world - 1 or loop else 0)
     eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
     if loop:
-        exchanger = LoopbackExchanger()
+        exchanger = LoopbackExchanger() if args.exchange == "loopback" else SelfP2PExchanger(0, 1)
         info = SlabInfo(0, 3, first, count)  # drives the multi-rank round structure
     else:
         exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
@@ -250,7 +256,8 @@ def main():
                 "grid": [gnx, gny, gnz],
                 "kernel": kname,
                 "parallelism": (f"z-slab x{world}" if not loop else
-                                "1 GPU rehearsing an interior rank (periodic loopback halo, two streams)") +
+                                "1 GPU rehearsing an interior rank (periodic halo, two streams, "
+                                + ("device copies)" if args.exchange == "loopback" else "RCCL send/recv to self)")) +
                                ("" if not multi or loop else
                                                      ", RCCL halo P2P overlapped" if args.exchange == "nccl"
                                                      else ", host-staged gloo halo (rehearsal)"),
@@ -284,7 +291,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or args.exchange == "nccl-self":
         dist.destroy_process_group()
 
 

@@ -87,6 +87,21 @@ class HostStagedExchanger(TorchDistExchanger):
         return []
 
 
+class SelfP2PExchanger(TorchDistExchanger):
+    """LoopbackExchanger's periodic halos, but through torch.distributed P2P
+    with this rank as its own peer (world size 1, RCCL): exercises the RCCL
+    send/recv path of TorchDistExchanger -- batch_isend_irecv posted on the
+    boundary stream, completion waited for on that stream -- on a one-GPU box
+    (bench.py --exchange nccl-self).  Sends and receives to one peer match in
+    posting order: send_hi -> recv_lo, send_lo -> recv_hi."""
+
+    def exchange(self, send_lo, send_hi, recv_lo, recv_hi):
+        me = self.rank
+        ops = [dist.P2POp(dist.isend, send_hi, me, self.group), dist.P2POp(dist.irecv, recv_lo, me, self.group),
+               dist.P2POp(dist.isend, send_lo, me, self.group), dist.P2POp(dist.irecv, recv_hi, me, self.group)]
+        return dist.batch_isend_irecv(ops)
+
+
 class LoopbackExchanger:
     """Rehearsal on ONE GPU of a rank with two neighbours: the slab's own
     boundary planes become its halos (periodic in z), copied device to device

@@ -135,3 +135,38 @@ def test_fused_needs_deep_halo(gpu):
     e.reset()
     with pytest.raises(_lib.StencilError):
         e.sweep2(e.a, e.b, 0, 8)
+
+
+def _periodic_run(gpu, exchanger, nx, ny, nz, it, shape="star"):
+    """SlabJacobi on one rank whose halos are its own boundary planes."""
+    from stencil_amd.slab import SlabInfo, SlabJacobi
+    spec = StencilSpec(dims=3, dtype="fp64", shape=shape)
+    fuse = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
+    spec = StencilSpec(dims=3, dtype="fp64", shape=shape, halo=max(2, fuse))
+    e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
+    slab = SlabJacobi(e, SlabInfo(0, 3, 0, nz), exchanger)
+    slab.init("random", 5, plane_elems=nx * ny)
+    slab.run(it)
+    torch.cuda.synchronize()
+    return e.interior(slab.cur).clone()
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+def test_rccl_self_p2p_matches_device_copies(gpu, shape):
+    """The RCCL send/recv path of the slab exchange (TorchDistExchanger's
+    batch_isend_irecv on the boundary stream, waited for on that stream), run
+    with this process as its own peer (world size 1), gives bit for bit the
+    result of the same periodic halos moved by device copies."""
+    import os
+    import torch.distributed as dist
+    from stencil_amd.slab import LoopbackExchanger, SelfP2PExchanger
+    nx, ny, nz, it = 70, 45, 33, 13
+    want = _periodic_run(gpu, LoopbackExchanger(), nx, ny, nz, it, shape)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29571" if shape == "star" else "29572"
+    dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), rank=0, world_size=1)
+    try:
+        got = _periodic_run(gpu, SelfP2PExchanger(0, 1), nx, ny, nz, it, shape)
+    finally:
+        dist.destroy_process_group()
+    assert torch.equal(got, want)
