@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-signal", action="store_true",
+                    help="multi-GPU rounds as separate boundary/interior launches (no face counters)")
     ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self"],
                     help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
     ap.add_argument("--share-device", action="store_true",
@@ -172,6 +174,7 @@ def main():
     else:
         exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
         info = SlabInfo(rank, world, first, count)
+    SlabJacobi.use_signal = not args.no_signal
     slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
     slab.init("reference")
     kernel_id = eng.plan(12)[1]
@@ -207,6 +210,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+    if multi and slab.signal_timeouts():
+        raise SystemExit("a face-counter wait timed out: the slab rounds did not complete")
     if multi:
         # Interior launch time for the roofline, from HIP events on the
         # interior stream over a few more rounds AFTER the timed region: the
@@ -224,7 +229,10 @@ def main():
     bytes_per_update = 2 * spec.elem_bytes
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
     edge = slab.depth if slab.fused else max(1, slab.depth)
-    cells_per_launch = cells_per_gpu if not multi else cells_per_gpu * (count - 2 * edge) / count
+    # the timed launch: the whole slab (single-GPU job, or face-signalled
+    # slab rounds) or the interior between the two boundary launches
+    whole = not multi or slab.signalled
+    cells_per_launch = cells_per_gpu if whole else cells_per_gpu * (count - 2 * edge) / count
     alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
     if not multi:
         # device time per `sweeps_per_launch` sweeps, charged pro rata (with
@@ -262,6 +270,9 @@ def main():
                                                      ", RCCL halo P2P overlapped" if args.exchange == "nccl"
                                                      else ", host-staged gloo halo (rehearsal)"),
                 "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
+                "rounds": (None if not multi else
+                           "one face-signalled launch per round" if slab.signalled else
+                           "boundary + interior launches per round"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -275,6 +286,8 @@ def main():
                 "mean_launch_ms": round(launch_ms, 5),
                 "launches": kernel_launches,
                 "launch_timing": ("hipEvents of stencil_iterate over the timed region" if not multi else
+                                  "events around the face-signalled whole-slab launches of extra rounds after the timed region"
+                                  if slab.signalled else
                                   "events around the interior launches of extra rounds after the timed region"),
             },
         }

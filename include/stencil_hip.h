@@ -185,6 +185,34 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
 int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
                    int32_t steps, void* stream);
 
+/* Multi-GPU slabs: stencil_sweepk over [begin, end) (3D 7-point star, steps
+ * 3..5) as ONE launch whose workgroups add 1 to counters[0] as soon as the
+ * low face planes [begin, begin+steps) are stored and to counters[1] for
+ * [end-steps, end) (the last z-chunk marches downward, so both faces come
+ * first); *signals_per_face = adds per face per launch.  counters: two
+ * uint32 in device memory, zeroed by the caller, accumulating over launches.
+ * face_signal (optional, from stencil_face_signal_create): the workgroup
+ * that completes a face's count for this launch also adds 1 to it, so it
+ * grows by 2 per launch once both faces are stored.
+ * stencil_wait_counters queues on `stream` a one-lane kernel that returns
+ * when counters[0] >= target_lo and counters[1] >= target_hi -- what is
+ * queued behind it (the halo send) waits for the faces, not for the whole
+ * launch.  After 10 s it sets *timeout_flag and returns instead.
+ * stencil_wait_face_signal queues the same wait on the command processor
+ * (hipStreamWaitValue64, *face_signal >= target): no kernel, no timeout. */
+int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                          int32_t steps, uint32_t* counters, uint64_t* face_signal, int32_t* signals_per_face,
+                          void* stream);
+int stencil_wait_counters(const uint32_t* counters, uint32_t target_lo, uint32_t target_hi, uint32_t* timeout_flag,
+                          void* stream);
+/* face signals: 8 bytes of HIP signal memory (hipExtMallocWithFlags,
+ * hipMallocSignalMemory) holding a uint64 count */
+int stencil_face_signal_create(uint64_t** face_signal);
+int stencil_face_signal_destroy(uint64_t* face_signal);
+int stencil_face_signal_reset(uint64_t* face_signal, void* stream);   /* queued: *face_signal = 0 */
+int stencil_face_signal_read(const uint64_t* face_signal, uint64_t* value);  /* synchronous */
+int stencil_wait_face_signal(const uint64_t* face_signal, uint64_t target, void* stream);
+
 /* Whole job: `iterations` ping-pong sweeps starting from grid `a` (grid `b`
  * must hold the same ghosts). *final_in_b = 1 when the result is in `b`
  * (iterations odd), 0 when in `a` (parity rule, stencil.cpp:88-92,134).

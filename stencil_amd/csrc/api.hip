@@ -195,6 +195,27 @@ __global__ void __launch_bounds__(256) plane_sums_kernel(const T* __restrict__ b
     if (threadIdx.x == 0) out[s] = red[0];
 }
 
+// One lane polls two face counters (agent-scope relaxed loads: they bypass
+// L1, MI355X_MICROARCH.md §visibility) until both reach their targets, so the
+// kernels queued behind it on its stream (the RCCL send of the faces) start
+// only then; the producers released before adding.  Gives up after 10 s of
+// s_memrealtime (100 MHz) and sets *timeout instead of holding the queue.
+__global__ void __launch_bounds__(64) wait_counters_kernel(const uint32_t* __restrict__ c, uint32_t tlo, uint32_t thi,
+                                                           uint32_t* __restrict__ timeout) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t a = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t b = __hip_atomic_load(&c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a >= tlo && b >= thi) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(1000) * 1000 * 1000) {
+            __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // Streaming copy used to calibrate attainable HBM bandwidth: 4 independent
 // 16-B loads in flight per lane, one pass, no grid-stride loop.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -415,6 +436,76 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
                        : launch_temporalk(*l, in, out, begin, end, steps, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();
     return rc;
+}
+
+int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                          int32_t steps, uint32_t* counters, uint64_t* face_signal, int32_t* signals_per_face,
+                          void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (!counters) return set_error(STENCIL_EINVAL, "null counters");
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range out of bounds");
+    if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
+    int nsig = 0;
+    const int rc = launch_tkstrip_signal(*l, in, out, begin, end, steps, counters,
+                                         reinterpret_cast<unsigned long long*>(face_signal), &nsig, as_stream(stream));
+    if (rc == STENCIL_OK) {
+        if (signals_per_face) *signals_per_face = nsig;
+        clear_error();
+    }
+    return rc;
+}
+
+int stencil_wait_counters(const uint32_t* counters, uint32_t target_lo, uint32_t target_hi, uint32_t* timeout_flag,
+                          void* stream) {
+    clear_error();
+    if (!counters || !timeout_flag) return set_error(STENCIL_EINVAL, "null counters / flag");
+    hipLaunchKernelGGL(wait_counters_kernel, dim3(1), dim3(64), 0, as_stream(stream), counters, target_lo, target_hi,
+                       timeout_flag);
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
+int stencil_face_signal_create(uint64_t** face_signal) {
+    clear_error();
+    if (!face_signal) return set_error(STENCIL_EINVAL, "null face_signal");
+    *face_signal = nullptr;
+    int dev = 0, ok = 0;
+    STENCIL_HIP_CHECK(hipGetDevice(&dev));
+    STENCIL_HIP_CHECK(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev));
+    if (!ok) return set_error(STENCIL_EUNSUPPORTED, "device cannot wait on stream values");
+    void* p = nullptr;
+    STENCIL_HIP_CHECK(hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory));
+    *face_signal = static_cast<uint64_t*>(p);
+    return STENCIL_OK;
+}
+
+int stencil_face_signal_destroy(uint64_t* face_signal) {
+    clear_error();
+    if (face_signal) STENCIL_HIP_CHECK(hipFree(face_signal));
+    return STENCIL_OK;
+}
+
+int stencil_face_signal_reset(uint64_t* face_signal, void* stream) {
+    clear_error();
+    if (!face_signal) return set_error(STENCIL_EINVAL, "null face_signal");
+    STENCIL_HIP_CHECK(hipStreamWriteValue64(as_stream(stream), face_signal, 0, 0));
+    return STENCIL_OK;
+}
+
+int stencil_face_signal_read(const uint64_t* face_signal, uint64_t* value) {
+    clear_error();
+    if (!face_signal || !value) return set_error(STENCIL_EINVAL, "null face_signal / value");
+    STENCIL_HIP_CHECK(hipMemcpy(value, face_signal, sizeof(uint64_t), hipMemcpyDefault));
+    return STENCIL_OK;
+}
+
+int stencil_wait_face_signal(const uint64_t* face_signal, uint64_t target, void* stream) {
+    clear_error();
+    if (!face_signal) return set_error(STENCIL_EINVAL, "null face_signal");
+    STENCIL_HIP_CHECK(hipStreamWaitValue64(as_stream(stream), const_cast<uint64_t*>(face_signal), target,
+                                           hipStreamWaitValueGte, ~uint64_t(0)));
+    return STENCIL_OK;
 }
 
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {

@@ -70,6 +70,8 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
                      int steps, hipStream_t s);
 int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                    int cfg, hipStream_t s);
+int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s);
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                 hipStream_t s);
 bool zmarch_supports(const stencil_problem& p);

@@ -37,6 +37,7 @@
 // kernels_temporalk.hip; intermediate planes keep ghost cells at their input
 // value; slab-halo planes (HALO_LO/HI) are advanced.  Bitwise equal to K
 // plain sweeps (tests/test_gpu_parity.py).
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -78,10 +79,22 @@ struct StripTile {
 
 // DIAG (timing experiments only, results are wrong): 1 = no loads after the
 // first two planes, 2 = no arithmetic (t_s = centre), 3 = no stores
-template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0>
+// SIG: face signalling for multi-GPU slabs (stencil_sweepk_signal): the
+// last z-chunk of every tile marches DOWNWARD, so the K planes of both faces
+// of the range are among the first planes stored, and the workgroup that
+// stores a face signals sig[0] (low face) / sig[1] (high face) right after
+// (release, then one agent-scope add: MI355X_MICROARCH.md §visibility).  A
+// stream waits for the counts (stencil_wait_counters) and sends the faces
+// while the rest of the launch runs.  With fsig (HIP signal memory), the
+// workgroup whose add completes a face's count for this launch (the counts
+// run on across launches: every tiles_x*tiles_y-th add) also adds 1 to
+// *fsig, so the command processor can gate the exchange stream on it
+// (hipStreamWaitValue64) with no wait kernel resident during the launch.
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
-                int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
+                int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
+                unsigned long long* __restrict__ fsig) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -97,10 +110,13 @@ __global__ void __launch_bounds__(64 * NW)
     const int nzr = zend - zbeg;
     const int64_t tiles = int64_t(tiles_x) * tiles_y;
     int64_t lo, hi;
+    bool rev = false;  // this workgroup's chunk marches down (SIG: the last chunk)
     if (zchunk > 0) {
         const int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
         lo = t * nzr + c * zchunk;
         hi = lo + (zchunk < nzr - c * zchunk ? zchunk : nzr - c * zchunk);
+        const int64_t nch = (nzr + zchunk - 1) / zchunk;
+        rev = SIG && nch >= 2 && c == nch - 1;
     } else {
         const int64_t units = tiles * nzr;
         lo = units * blockIdx.x / gridDim.x;
@@ -128,7 +144,8 @@ __global__ void __launch_bounds__(64 * NW)
     // neighbour strips (the first / last wave reads its own: those rows are ring rows)
     const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
 
-    while (lo < hi) {  // one segment: tile t, planes [za, zb)
+    auto segment = [&](auto REV_) {  // one segment: tile t, planes [za, zb)
+    constexpr bool REV = decltype(REV_)::value;
     const int t = int(lo / nzr);
     const int za = zbeg + int(lo - int64_t(t) * nzr);
     const int zb = za + (hi - lo < int64_t(zend - za) ? int(hi - lo) : zend - za);
@@ -161,9 +178,13 @@ __global__ void __launch_bounds__(64 * NW)
     }
     const int ld_lo = halo_lo ? -K : -1;
     const int ld_hi = halo_hi ? nz + K - 1 : nz;
+    const int zfirst = za - K > ld_lo ? za - K : ld_lo;
     const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
-    auto load_plane = [&](VT (&d)[RY], int z) {
-        const int zz = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
+    // march index m -> plane: the chunk is walked upward, or downward (REV)
+    auto zr = [&](int m) { return REV ? za + zb - 1 - m : m; };
+    auto load_plane = [&](VT (&d)[RY], int m) {
+        const int z = zr(m);
+        const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
         for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
@@ -202,14 +223,14 @@ __global__ void __launch_bounds__(64 * NW)
         bool zin[K];
 #pragma unroll
         for (int s = 1; s <= K; ++s) {
-            const int z = p - s;
+            const int z = zr(p - s);
             const int lo_s = halo_lo ? -(K - s) : 0;
             const int hi_s = halo_hi ? nz + (K - s) : nz;
             zin[s - 1] = z >= lo_s && z < hi_s;
         }
         const int zo = p - K;  // t_K(p-K) -> HBM
         const bool do_store = DIAG != 3 && zo >= za && zo < zb;
-        char* obase = dst + int64_t(zo) * plane * int64_t(sizeof(T));
+        char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             VT prev{};  // this row's result of the previous stage
@@ -238,8 +259,10 @@ __global__ void __launch_bounds__(64 * NW)
                     T sum = (j == 0 ? wl : c[j - 1]) + (j == V - 1 ? er : c[j + 1]);
                     sum += up[j];
                     sum += dn[j];
-                    sum += zm[j];
-                    sum += zp[j];
+                    // the reference adds the lower plane first; marching down,
+                    // the march's z+ is the lower one
+                    sum += REV ? zp[j] : zm[j];
+                    sum += REV ? zm[j] : zp[j];
                     o[j] = DIAG == 2 ? c[j] : sfma0(sum, avg);
                     if (s < K) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
                 }
@@ -274,6 +297,37 @@ __global__ void __launch_bounds__(64 * NW)
             *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = H[s - 2][(S - s + 5) & 1][0];
             *reinterpret_cast<VT*>(&L[P][s - 1][w][1][xl]) = H[s - 2][(S - s + 5) & 1][RY - 1];
         }
+        if constexpr (SIG) {
+            // right after the store of a face's last plane (the host makes
+            // every chunk at least K planes long): the low face is planes
+            // [zbeg, zbeg+K) of the first chunk, the high face [zend-K, zend)
+            // of the last one, walked down (REV) so they come first.  Uniform
+            // condition: every wave drains its stores, then one lane releases
+            // and adds.
+            const bool lo_here = !REV && za == zbeg && zo == za + K - 1;
+            const bool hi_here = zb == zend && zo == (REV ? za + K - 1 : zb - 1);
+            if (lo_here || hi_here) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0 && threadIdx.y == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const unsigned ntiles = unsigned(tiles_x) * unsigned(tiles_y);
+                    bool last = false;
+                    if (lo_here)
+                        last |= (__hip_atomic_fetch_add(&sig[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (hi_here)
+                        last |= (__hip_atomic_fetch_add(&sig[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (fsig && last) {
+                        // every add of this face came after its workgroup's release
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __hip_atomic_fetch_add(fsig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+            }
+        }
         if constexpr (DIAG != 1) load_plane(vin[(S + 2) & 3], p + 2);  // slot of in(p-2), consumed above
     };
 
@@ -288,7 +342,15 @@ __global__ void __launch_bounds__(64 * NW)
     if (p <= plast) step(std::integral_constant<int, 0>{}, p);
     if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
     if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
-    }  // segments
+    };  // segment
+    while (lo < hi) {
+        if constexpr (SIG) {
+            if (rev) segment(std::true_type{});
+            else segment(std::false_type{});
+        } else {
+            segment(std::false_type{});
+        }
+    }
 }
 
 int senv_int(const char* name, int dflt) {
@@ -296,8 +358,9 @@ int senv_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0>
-int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
+template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false>
+int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
+              unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
@@ -306,7 +369,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG>;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG>;
     const int64_t tiles = gx * gy;
     int zc = senv_int("STENCIL_TK_ZCHUNK", 0);
     int64_t nb = 0;
@@ -322,7 +385,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
                 return set_error(STENCIL_EHIP, "occupancy query failed");
             slots = std::max(1, cus * std::max(1, per_cu));
         }
-        if (senv_int("STENCIL_TK_BALANCE", 0)) {
+        if (!SIG && senv_int("STENCIL_TK_BALANCE", 0)) {
             // one equal share of the (tile, z) units per slot, each share at
             // least 4K planes long (a segment costs 2K planes of pipeline fill).
             // Measured 20-30 % SLOWER than whole chunks on MI355X (512^3 fp64
@@ -341,18 +404,48 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
                 const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 2 * K);
                 if (cost <= best) best = cost, best_c = c;
             }
+            // A slab of a multi-GPU job (halo flags): its halo exchange runs
+            // kernels (RCCL P2P, or the face wait) beside this launch, and a
+            // grid that fills every CU for several rounds loses a whole round
+            // of balance to one busy CU: 512^3 fp64 K=4, 990 workgroups
+            // 0.50 -> 0.565 ms with a 1-wave kernel resident on another queue
+            // (tools/sig_time.py), 220 workgroups (2 chunks) 0.48 either way.
+            // So: the most chunks that still fit one round with a CU per XCD
+            // to spare, when the tiles fit at all.
+            if (l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI)) {
+                const int64_t room = slots - slots / 32;
+                for (int64_t c = 1; tiles * c <= room && c <= nz; ++c) {
+                    if (c > 1 && (nz + c - 1) / c < 2 * K) break;
+                    best_c = c;
+                }
+            }
             zc = int((nz + best_c - 1) / best_c);
             nb = tiles * ((nz + zc - 1) / zc);
         }
     }
+    if constexpr (SIG) {
+        // every chunk at least K planes (a face lies inside one chunk)
+        int64_t nch = (nz + zc - 1) / zc;
+        auto last = [&](int64_t c) { return nz - (c - 1) * ((nz + c - 1) / c); };
+        while (nch > 1 && ((nz + nch - 1) / nch < K || last(nch) < K)) --nch;
+        zc = int((nz + nch - 1) / nch);
+        nb = tiles * nch;
+        if (nsig) *nsig = int(tiles);
+    }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
+    if (senv_int("STENCIL_TK_VERBOSE", 0)) {
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0);
+        std::fprintf(stderr, "tkstrip K=%d V=%d RY=%d NW=%d: tiles %lldx%lld, zchunk %d, %lld workgroups, %d per CU\n", K,
+                     V, RY, NW, (long long)gx, (long long)gy, zc, (long long)nb, per_cu);
+    }
     const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
     if ((lo || hi) && l.zghost < K)
         return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
                          (long long)l.zghost);
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       avg_weight<T>(l.prob));
+                       avg_weight<T>(l.prob), sig, fsig);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
@@ -418,6 +511,29 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
         }
     }
     return set_error(STENCIL_EINVAL, "tkstrip steps must be 3, 4 or 5 (got %d)", steps);
+}
+
+// The default shapes with face signalling (stencil_sweepk_signal).
+int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s) {
+    if (!temporal2_supports(l.prob))
+        return set_error(STENCIL_EUNSUPPORTED, "face-signalled sweeps cover the 3D r=1 naive 7-point star only");
+    if (l.prob.dtype == STENCIL_F32) {
+        switch (steps) {
+        case 3: return launch_st<float, 4, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 4: return launch_st<float, 2, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 5: return launch_st<float, 2, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        default: break;
+        }
+    } else {
+        switch (steps) {
+        case 3: return launch_st<double, 2, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 4: return launch_st<double, 1, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 5: return launch_st<double, 1, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        default: break;
+        }
+    }
+    return set_error(STENCIL_EINVAL, "face-signalled sweeps: steps must be 3, 4 or 5 (got %d)", steps);
 }
 
 }  // namespace stencil

@@ -116,6 +116,36 @@ class JacobiEngine:
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
                                            _stream_handle(stream)), "stencil_sweepk")
 
+    @property
+    def supports_signal(self) -> bool:
+        """Face-signalled K-step launches (stencil_sweepk_signal): 3D 7-point star."""
+        s = self.spec
+        return (s.dims == 3 and s.shape == "star" and s.radius == 1 and s.order == "naive" and self.fused
+                and 3 <= self.fuse_steps <= 5)
+
+    def sweepk_signal(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int,
+                      counters: torch.Tensor, stream=None, face_signal: "FaceSignal | None" = None) -> int:
+        """sweepk over [begin, end) as one launch that adds to counters[0] / [1]
+        once the low / high face planes are stored; returns adds per face.
+        With face_signal, it also grows by 2 once both faces are complete."""
+        n = ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_sweepk_signal(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
+                                                  ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
+                                                  ctypes.c_void_p(counters.data_ptr()),
+                                                  face_signal.ptr if face_signal is not None else None,
+                                                  ctypes.byref(n), _stream_handle(stream)), "stencil_sweepk_signal")
+        return int(n.value)
+
+    def face_signal(self) -> "FaceSignal":
+        return FaceSignal()
+
+    def wait_counters(self, counters: torch.Tensor, target_lo: int, target_hi: int, stream=None) -> None:
+        """Queue on `stream` a wait until counters[0] >= target_lo and
+        counters[1] >= target_hi (counters[2] is set on a 10 s timeout)."""
+        _lib.check(self.lib.stencil_wait_counters(ctypes.c_void_p(counters.data_ptr()), target_lo, target_hi,
+                                                  ctypes.c_void_p(counters.data_ptr() + 8), _stream_handle(stream)),
+                   "stencil_wait_counters")
+
     def iterate(self, iterations: int, stream=None, timed: bool = False):
         """Whole job a -> ... ; returns (final grid tensor, device ms or None)."""
         fin = ctypes.c_int(0)
@@ -170,6 +200,40 @@ class JacobiEngine:
                                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                                _stream_handle(stream)), "stencil_plane_sums")
         return out
+
+
+class FaceSignal:
+    """A uint64 count in HIP signal memory that stencil_sweepk_signal bumps
+    once per completed face and a stream can wait on in the command
+    processor (stencil_wait_face_signal): no wait kernel on the GPU."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.ptr = ctypes.c_void_p()
+        _lib.check(self.lib.stencil_face_signal_create(ctypes.byref(self.ptr)), "stencil_face_signal_create")
+
+    def reset(self, stream=None) -> None:
+        _lib.check(self.lib.stencil_face_signal_reset(self.ptr, _stream_handle(stream)), "stencil_face_signal_reset")
+
+    def wait(self, target: int, stream=None) -> None:
+        _lib.check(self.lib.stencil_wait_face_signal(self.ptr, ctypes.c_uint64(target), _stream_handle(stream)),
+                   "stencil_wait_face_signal")
+
+    def value(self) -> int:
+        v = ctypes.c_uint64(0)
+        _lib.check(self.lib.stencil_face_signal_read(self.ptr, ctypes.byref(v)), "stencil_face_signal_read")
+        return int(v.value)
+
+    def close(self) -> None:
+        if self.ptr and self.ptr.value:
+            self.lib.stencil_face_signal_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def copy_bandwidth(nbytes: int, reps: int = 20, device: int = 0) -> float:

@@ -146,6 +146,19 @@ class SlabJacobi:
         self.on_gpu = self.cur.device.type == "cuda"
         self._timing = None  # list of (start, end) events around interior sweeps
         self._ev_bnd = self._ev_int = None  # last round's boundary / interior completion
+        # Face-signalled rounds (_round_signal): one launch per round whose
+        # face-owning workgroups signal device counters [lo, hi, timeout].
+        self.signalled = (self.on_gpu and self.fused and overlap and slab.world > 1 and n >= 2 * self.k
+                          and bool(getattr(backend, "supports_signal", False)) and self.use_signal)
+        self._sig = torch.zeros(4, dtype=torch.int32, device=self.cur.device) if self.signalled else None
+        self._sig_rounds = 0
+        # the exchange stream waits for the faces in the command processor
+        # (FaceSignal, hipStreamWaitValue64) where the backend has it, else
+        # through a one-lane wait kernel -- which, resident beside the launch,
+        # measured ~10 % slower launches (tools/sig_time.py)
+        self._fsig = None
+        if self.signalled and self.use_face_signal and hasattr(backend, "face_signal"):
+            self._fsig = backend.face_signal()
         if self.on_gpu:
             # The boundary stream has the high priority, so the boundary
             # planes and their exchange come first and stay off the critical
@@ -241,6 +254,57 @@ class SlabJacobi:
                 for w in self.ex.exchange(*self._halo_views(dst)):
                     w.wait()  # sa waits for the P2P
         self.cur, self.nxt = dst, src
+
+    def _round_signal(self) -> None:
+        """One K-step round as ONE launch over the whole slab (GPU, fused):
+        its first z-chunk marches up and its last down, so the face planes
+        are among the first it stores, and the workgroups that store them
+        add to device counters (stencil_sweepk_signal).  The exchange stream
+        queues a wait for the counts, then the P2P -- the faces leave while
+        the rest of the launch runs, with no separate boundary launches.
+        Dependencies: launch(r) reads the halos exchange(r-1) received (sb
+        waits for it); exchange(r) receives into the planes launch(r-1) read
+        as halos -- ordered because launch(r) only starts, and only signals,
+        after launch(r-1) (one stream)."""
+        src, dst = self.cur, self.nxt
+        n, k = self.slab.count, self.k
+        sa, sb = self.stream_bnd, self.stream_int
+        if self._ev_bnd is None:
+            main = torch.cuda.current_stream()
+            sa.wait_stream(main)
+            sb.wait_stream(main)
+        else:
+            sb.wait_event(self._ev_bnd)
+        with torch.cuda.stream(sb):
+            if self._timing is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record(sb)
+            nsig = self.be.sweepk_signal(src, dst, 0, n, k, self._sig, stream=sb, face_signal=self._fsig)
+            if self._timing is not None:
+                ev1.record(sb)
+                self._timing.append((ev0, ev1))
+            self._ev_int = torch.cuda.Event()
+            self._ev_int.record(sb)
+        self._sig_rounds += 1
+        target = self._sig_rounds * nsig
+        with torch.cuda.stream(sa):
+            if self._fsig is not None:
+                self._fsig.wait(2 * self._sig_rounds, stream=sa)
+            else:
+                self.be.wait_counters(self._sig, target, target, stream=sa)
+            for w in self.ex.exchange(*self._halo_views(dst)):
+                w.wait()  # sa waits for the P2P
+            self._ev_bnd = torch.cuda.Event()
+            self._ev_bnd.record(sa)
+        self.cur, self.nxt = dst, src
+
+    def signal_timeouts(self) -> int:
+        """Nonzero if a face-counter wait gave up (10 s): results invalid."""
+        if self._sig is None:
+            return 0
+        torch.cuda.synchronize(self.cur.device)
+        return int(self._sig[2].item())
 
     def finish(self) -> None:
         """Join the round streams into the caller's stream (after run())."""
@@ -350,13 +414,24 @@ class SlabJacobi:
         return "single"
 
     split2 = True  # allow the communication-avoiding 2-sweep rounds
+    use_signal = True  # face-signalled single-launch rounds where the backend has them
+    use_face_signal = True  # ... waited for in the command processor, not by a wait kernel
 
     def run(self, iterations: int) -> None:
         mode = self.mode
         if mode == "fused":
             k = self.k
+            if self.signalled and iterations >= k:
+                self.finish()
+                self._sig.zero_()  # on the caller's stream, before the rounds join it
+                if self._fsig is not None:
+                    self._fsig.reset()
+                self._sig_rounds = 0
             for _ in range(iterations // k):
-                self._stepk(k) if k != 2 else self._step2()
+                if self.signalled:
+                    self._round_signal()
+                else:
+                    self._stepk(k) if k != 2 else self._step2()
             rem = iterations % k
             if rem >= 2:
                 self._step2()
