@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-signal", action="store_true",
                     help="multi-GPU rounds as separate boundary/interior launches (no face counters)")
+    ap.add_argument("--face-signal", action="store_true",
+                    help="face-signalled rounds gated by hipStreamWaitValue64 on a signal word, not the wait kernel")
     ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self"],
                     help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
     ap.add_argument("--share-device", action="store_true",
@@ -175,6 +177,7 @@ def main():
         exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
         info = SlabInfo(rank, world, first, count)
     SlabJacobi.use_signal = not args.no_signal
+    SlabJacobi.use_face_signal = args.face_signal
     slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
     slab.init("reference")
     kernel_id = eng.plan(12)[1]

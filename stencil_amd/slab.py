@@ -152,10 +152,11 @@ class SlabJacobi:
                           and bool(getattr(backend, "supports_signal", False)) and self.use_signal)
         self._sig = torch.zeros(4, dtype=torch.int32, device=self.cur.device) if self.signalled else None
         self._sig_rounds = 0
-        # the exchange stream waits for the faces in the command processor
-        # (FaceSignal, hipStreamWaitValue64) where the backend has it, else
-        # through a one-lane wait kernel -- which, resident beside the launch,
-        # measured ~10 % slower launches (tools/sig_time.py)
+        # the exchange stream waits for the faces through the one-lane wait
+        # kernel (stencil_wait_counters, 10 s timeout) or, with
+        # use_face_signal, hipStreamWaitValue64 on a signal word -- which HIP
+        # also runs as a kernel (__amd_rocclr_streamOpsWait in the trace,
+        # profiles/r01j_sig_kernel_stats.csv) and which never times out
         self._fsig = None
         if self.signalled and self.use_face_signal and hasattr(backend, "face_signal"):
             self._fsig = backend.face_signal()
@@ -415,7 +416,7 @@ class SlabJacobi:
 
     split2 = True  # allow the communication-avoiding 2-sweep rounds
     use_signal = True  # face-signalled single-launch rounds where the backend has them
-    use_face_signal = True  # ... waited for in the command processor, not by a wait kernel
+    use_face_signal = False  # wait on the HIP signal word (hipStreamWaitValue64) instead of the counters
 
     def run(self, iterations: int) -> None:
         mode = self.mode

@@ -239,12 +239,13 @@ def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=Tru
     spec = StencilSpec(dims=3, dtype="fp64", halo=max(2, fuse))
     e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
     SlabJacobi.use_signal = signalled
+    default_fs = SlabJacobi.use_face_signal
     SlabJacobi.use_face_signal = face_signal
     try:
         slab = SlabJacobi(e, SlabInfo(0, 3, 0, nz), exchanger)
     finally:
         SlabJacobi.use_signal = True
-        SlabJacobi.use_face_signal = True
+        SlabJacobi.use_face_signal = default_fs
     assert slab.signalled == signalled
     assert (slab._fsig is not None) == (signalled and face_signal)
     slab.init("random", 5, plane_elems=nx * ny)
