@@ -22,7 +22,7 @@ HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
 
 all: $(LIB) $(CLI) oracle
 
-build/obj/%.o: stencil_amd/csrc/%.hip stencil_amd/csrc/common.hpp include/stencil_hip.h
+build/obj/%.o: stencil_amd/csrc/%.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

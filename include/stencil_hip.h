@@ -96,8 +96,14 @@ enum {
     STENCIL_KERNEL_DIRECT = 1,    /* one cell per lane, neighbours via L1/L2 */
     STENCIL_KERNEL_ZMARCH = 2,    /* 2.5D: LDS plane + z register queue */
     STENCIL_KERNEL_TEMPORAL2 = 3, /* ZMARCH with 2 fused time steps per launch */
-    STENCIL_KERNEL_TEMPORALK = 4  /* 3D 7-point star: K = 3..5 fused steps per launch
+    STENCIL_KERNEL_TEMPORALK = 4, /* 3D 7-point star: K = 3..5 fused steps per launch
                                      (K = env STENCIL_TK_STEPS, default 4) */
+    STENCIL_KERNEL_PERSISTENT = 5 /* 2D star r <= 2: the whole job in one launch, one
+                                     resident workgroup per tile, K-cell rings exchanged
+                                     through the grid with neighbour-only flags every
+                                     K sweeps (K = env STENCIL_TB2DP_K, default 8/r);
+                                     grids whose tiles do not all fit at once use
+                                     TEMPORAL2 */
 };
 enum { STENCIL_INIT_REFERENCE = 0, STENCIL_INIT_RANDOM = 1 };
 /* stencil_problem.flags: which z faces of this grid are halos filled by a

@@ -17,12 +17,12 @@ STENCIL_OK = 0
 F32, F64 = 0, 1
 STAR, BOX = 0, 1
 ORDER_NAIVE, ORDER_DMA = 0, 1
-KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2, KERNEL_TEMPORALK = 0, 1, 2, 3, 4
+KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2, KERNEL_TEMPORALK, KERNEL_PERSISTENT = 0, 1, 2, 3, 4, 5
 INIT_REFERENCE, INIT_RANDOM = 0, 1
 HALO_LO, HALO_HI = 1, 2
 
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2,
-                "temporalk": KERNEL_TEMPORALK}
+                "temporalk": KERNEL_TEMPORALK, "persistent": KERNEL_PERSISTENT}
 
 # Every symbol include/stencil_hip.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (

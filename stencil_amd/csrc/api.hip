@@ -48,7 +48,7 @@ int check_problem(const stencil_problem* p) {
     if (p->order != STENCIL_ORDER_NAIVE && p->order != STENCIL_ORDER_DMA) return set_error(STENCIL_EINVAL, "bad order %d", p->order);
     if (p->order == STENCIL_ORDER_DMA && (p->dims != 2 || p->shape != STENCIL_STAR))
         return set_error(STENCIL_EINVAL, "DMA sum order is defined for 2D star stencils only");
-    if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_TEMPORALK) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
+    if (p->kernel < STENCIL_KERNEL_AUTO || p->kernel > STENCIL_KERNEL_PERSISTENT) return set_error(STENCIL_EINVAL, "bad kernel %d", p->kernel);
     if (p->nx < 0 || p->ny < 0 || p->nz < 0) return set_error(STENCIL_EINVAL, "negative extent");
     if (p->dims == 2 && p->nz != 1) return set_error(STENCIL_EINVAL, "2D problems need nz = 1");
     if (p->halo < 0 || (p->halo > 0 && p->halo < p->radius) || p->halo > 64)
@@ -62,6 +62,8 @@ int check_problem(const stencil_problem* p) {
                          "TEMPORAL2 kernels cover 3D r=1 naive star/box and 2D star r<=4 only");
     if (p->kernel == STENCIL_KERNEL_TEMPORALK && !temporal2_supports(*p))
         return set_error(STENCIL_EUNSUPPORTED, "TEMPORALK kernels cover the 3D r=1 naive 7-point star only");
+    if (p->kernel == STENCIL_KERNEL_PERSISTENT && !tb2dp_supports(*p))
+        return set_error(STENCIL_EUNSUPPORTED, "the PERSISTENT kernel covers 2D star stencils with r <= 2 only");
     return STENCIL_OK;
 }
 
@@ -114,9 +116,19 @@ int iterate_tk_steps(const stencil_problem& p) {
 // (kernels_tb2d.hip) unless a single-sweep family is forced.
 bool iterate_tb2d(const stencil_problem& p) {
     if (!tb2d_supports(p)) return false;
-    if (p.kernel == STENCIL_KERNEL_TEMPORAL2) return true;
+    if (p.kernel == STENCIL_KERNEL_TEMPORAL2 || p.kernel == STENCIL_KERNEL_PERSISTENT) return true;
     const char* e = std::getenv("STENCIL_NO_T2");
     return p.kernel == STENCIL_KERNEL_AUTO && !(e && *e && *e != '0');
+}
+
+// The whole 2D job as one persistent launch (kernels_tb2dp.hip): explicit
+// PERSISTENT, or AUTO when STENCIL_TB2DP=1.  Falls back to the K-step launches
+// when the tiles do not all fit on the GPU at once.
+bool iterate_persistent(const stencil_problem& p) {
+    if (!tb2dp_supports(p)) return false;
+    if (p.kernel == STENCIL_KERNEL_PERSISTENT) return true;
+    const char* e = std::getenv("STENCIL_TB2DP");
+    return p.kernel == STENCIL_KERNEL_AUTO && iterate_tb2d(p) && e && *e == '1';
 }
 
 int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
@@ -510,6 +522,11 @@ int stencil_wait_face_signal(const uint64_t* face_signal, uint64_t target, void*
 
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches, int32_t* kernel) {
     if (int rc = check_layout(l)) return rc;
+    if (iterate_persistent(l->prob) && tb2dp_fits(*l)) {
+        if (launches) *launches = iterations ? 1 : 0;
+        if (kernel) *kernel = STENCIL_KERNEL_PERSISTENT;
+        return STENCIL_OK;
+    }
     if (iterate_tb2d(l->prob)) {
         const int64_t k = tb2d_max_steps(l->prob);
         if (launches) *launches = (int64_t(iterations) + k - 1) / k;
@@ -547,7 +564,18 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
     void* out = b;
     uint32_t i = 0;
     int rc = STENCIL_OK;
-    if (iterate_tb2d(l->prob)) {
+    if (iterate_persistent(l->prob)) {
+        int fin = 0;
+        rc = launch_tb2dp(*l, a, b, iterations, s, &fin);
+        if (rc == STENCIL_OK) {
+            i = iterations;
+            if (fin) std::swap(in, out);  // `in` names the grid holding the result
+        } else if (rc == STENCIL_EUNSUPPORTED) {
+            rc = STENCIL_OK;  // tiles do not fit at once: K-step launches below
+            clear_error();
+        }
+    }
+    if (iterate_tb2d(l->prob) && rc == STENCIL_OK) {
         const uint32_t k = uint32_t(tb2d_max_steps(l->prob));
         for (; i < iterations && rc == STENCIL_OK;) {
             const uint32_t n2 = std::min(k, iterations - i);

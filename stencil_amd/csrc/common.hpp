@@ -80,6 +80,12 @@ int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t beg
                  int steps, hipStream_t s);
 bool box27_supports(const stencil_problem& p);
 int launch_tb2d(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s);
+// the whole 2D job as one persistent launch (kernels_tb2dp.hip); EUNSUPPORTED
+// when the tiles do not all fit on the GPU at once
+int launch_tb2dp(const stencil_layout& l, void* a, void* b, uint32_t iterations, hipStream_t s, int* final_in_b);
+bool tb2dp_supports(const stencil_problem& p);
+bool tb2dp_fits(const stencil_layout& l);  // queries the current device
+int tb2dp_steps(const stencil_problem& p);
 bool tb2d_supports(const stencil_problem& p);
 int tb2d_max_steps(const stencil_problem& p);
 

@@ -115,8 +115,8 @@ auto ProgramOptions::parse(int argc, char** argv) -> std::optional<ProgramOption
              default: return false;
              }
          }},
-        {0, "kernel", Kind::Str, false, "[ext] GPU kernel family: auto, direct, zmarch, temporal2, temporalk.",
-         [&](const std::string& v) { if (v != "auto" && v != "direct" && v != "zmarch" && v != "temporal2" && v != "temporalk") return false; r.kernel = v; return true; }},
+        {0, "kernel", Kind::Str, false, "[ext] GPU kernel family: auto, direct, zmarch, temporal2, temporalk, persistent.",
+         [&](const std::string& v) { if (v != "auto" && v != "direct" && v != "zmarch" && v != "temporal2" && v != "temporalk" && v != "persistent") return false; r.kernel = v; return true; }},
         {0, "device", Kind::Int, false, "[ext] HIP device index.",
          [&](const std::string& v) { int64_t d; if (!parse_i64(v, d) || d < 0) return false; r.device = int(d); return true; }},
         {0, "init", Kind::Str, false, "[ext] Initial interior: reference (zeros) or random.",

@@ -33,7 +33,7 @@ struct ProgramOptions {
     int64_t nx = -1, ny = -1, nz = -1;  // --nx/--ny/--nz (default: matrix_size)
     bool fp64 = false;             // --dtype fp32|fp64 (reference: fp32)
     bool box = false;              // --shape star|box
-    std::string kernel = "auto";   // --kernel auto|direct|zmarch|temporal2
+    std::string kernel = "auto";   // --kernel auto|direct|zmarch|temporal2|temporalk|persistent
     int device = 0;                // --device N
     bool random_init = false;      // --init reference|random
     uint64_t seed = 0x5EED;        // --seed N

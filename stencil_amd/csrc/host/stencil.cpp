@@ -25,6 +25,7 @@ int kernel_of(const std::string& k) {
     if (k == "zmarch") return STENCIL_KERNEL_ZMARCH;
     if (k == "temporal2") return STENCIL_KERNEL_TEMPORAL2;
     if (k == "temporalk") return STENCIL_KERNEL_TEMPORALK;
+    if (k == "persistent") return STENCIL_KERNEL_PERSISTENT;
     return STENCIL_KERNEL_AUTO;
 }
 
@@ -96,6 +97,7 @@ auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGri
     case HIP_ZMARCH: p.kernel = STENCIL_KERNEL_ZMARCH; break;
     case HIP_TEMPORAL2: p.kernel = STENCIL_KERNEL_TEMPORAL2; break;
     case HIP_TEMPORALK: p.kernel = STENCIL_KERNEL_TEMPORALK; break;
+    case HIP_PERSISTENT: p.kernel = STENCIL_KERNEL_PERSISTENT; break;
     case HIP: p.kernel = kernel_of(options.kernel); break;
     default: p.kernel = STENCIL_KERNEL_AUTO; break;
     }
@@ -194,6 +196,7 @@ auto Stencil::run(std::string_view method_name) -> std::optional<std::chrono::st
         {"HIPZMarch", HIP_ZMARCH},
         {"HIPTemporal2", HIP_TEMPORAL2},
         {"HIPTemporalK", HIP_TEMPORALK},
+        {"HIPPersistent", HIP_PERSISTENT},
     };
     auto const iter = method_map.find(method_name);
     if (iter == method_map.end()) return std::nullopt;

@@ -30,6 +30,7 @@ public:
         HIP_ZMARCH,         ///< naive order, 2.5D LDS/register z-marching kernel (3D r=1)
         HIP_TEMPORAL2,      ///< naive order, two fused time steps per launch
         HIP_TEMPORALK,      ///< naive order, 3 or 4 fused time steps per launch (7-point star)
+        HIP_PERSISTENT,     ///< naive order, the whole 2D job in one launch (neighbour flags)
     };
 
     Stencil() = default;

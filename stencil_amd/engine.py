@@ -29,7 +29,7 @@ class StencilSpec:
     shape: str = "star"          # "star" | "box"
     radius: int = 1
     order: str = "naive"         # "naive" | "dma"
-    kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2" | "temporalk"
+    kernel: str = "auto"         # "auto" | "direct" | "zmarch" | "temporal2" | "temporalk" | "persistent"
     halo: int = 0                # 3D ghost planes per z side (0 = radius); 2 for fused slabs
 
     def problem(self, nx: int, ny: int, nz: int, flags: int = 0) -> _lib.Problem:

@@ -102,6 +102,56 @@ def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
         assert same_bits(got, want), (nx, ny, it)
 
 
+@pytest.mark.parametrize("k", ["1", "3", "8", "12"])
+@pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma")])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_2d_persistent(gpu, monkeypatch, k, r, order, dtype):
+    """kernels_tb2dp.hip: the whole job in one cooperative launch, K-sweep
+    blocks between neighbour-flag waits; ragged grids, iteration counts below,
+    at and between multiples of K, zero iterations; a K whose ring does not fit
+    the region falls back to the K-step launches."""
+    from stencil_amd import _lib
+    monkeypatch.setenv("STENCIL_TB2DP_K", k)
+    kk = min(int(k), 24 // r)
+    fits_region = 128 - 2 * kk * r >= max(4, kk * r) and 64 - 2 * kk * r >= max(4, kk * r)
+    for nx, ny, it in ((301, 170, 11), (5, 3, 4), (64, 200, 9), (257, 129, 1), (130, 66, 2 * kk), (40, 40, 0)):
+        p = ob.problem(2, dtype, "star", r, order, nx, ny)
+        want = ob.run(p, it, "random", 8 + r)
+        e, got = gpu_run(gpu, 2, dtype, "star", r, order, "persistent", nx, ny, 1, it, "random", 8 + r)
+        assert same_bits(got, want), (nx, ny, it)
+        launches, kernel = e.plan(it)
+        if fits_region and it:
+            assert (launches, kernel) == (1, _lib.KERNEL_PERSISTENT)
+        else:
+            assert kernel != _lib.KERNEL_PERSISTENT or it == 0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("order", ["naive", "dma"])
+def test_c1_persistent(gpu, dtype, order):
+    """BASELINE config 1 through the persistent kernel: one launch, bitwise the
+    oracle (and the probe's golden sum for the naive order)."""
+    from stencil_amd import _lib
+    p = ob.problem(2, dtype, "star", 1, order, 1024, 1024)
+    want = ob.run(p, 100, threads=8)
+    e, got = gpu_run(gpu, 2, dtype, "star", 1, order, "persistent", 1024, 1024, 1, 100)
+    assert e.plan(100) == (1, _lib.KERNEL_PERSISTENT)
+    assert same_bits(got, want)
+    if order == "naive":
+        sums = {"fp32": 10520.714292108827, "fp64": 10520.714308906061}
+        assert ob.interior_sum(p, got) == pytest.approx(sums[dtype], rel=1e-15, abs=0)
+
+
+def test_persistent_too_large_falls_back(gpu):
+    """More tiles than resident workgroups: the K-step launches run instead."""
+    from stencil_amd import _lib
+    p = ob.problem(2, "fp64", "star", 1, "naive", 8000, 6000)
+    want = ob.run(p, 3, "random", 3, threads=8)
+    e, got = gpu_run(gpu, 2, "fp64", "star", 1, "naive", "persistent", 8000, 6000, 1, 3, "random", 3)
+    assert e.plan(3)[1] != _lib.KERNEL_PERSISTENT
+    assert same_bits(got, want)
+
+
 # ------------------------------------------------------- 3D hot kernels
 @pytest.mark.parametrize("stencil", ["star", "box"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
@@ -435,6 +485,10 @@ def test_cli_check_result_on_gpu(gpu):
                          timeout=300)
     assert out.returncode == 0, out.stderr + out.stdout
     assert out.stdout.count("is correct.") == 3
+    out = subprocess.run([cli, "-s", "300", "-b", "1", "-i", "37", "-m", "HIPPersistent", "HIPTemporal2", "-c"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr + out.stdout
+    assert out.stdout.count("is correct.") == 2
 
 
 def test_cli_block_reach(gpu):
