@@ -528,7 +528,7 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
         return STENCIL_OK;
     }
     if (iterate_tb2d(l->prob)) {
-        const int64_t k = tb2d_max_steps(l->prob);
+        const int64_t k = tb2d_steps(*l, iterations);
         if (launches) *launches = (int64_t(iterations) + k - 1) / k;
         if (kernel) *kernel = STENCIL_KERNEL_TEMPORAL2;
         return STENCIL_OK;
@@ -576,7 +576,7 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         }
     }
     if (iterate_tb2d(l->prob) && rc == STENCIL_OK) {
-        const uint32_t k = uint32_t(tb2d_max_steps(l->prob));
+        const uint32_t k = uint32_t(tb2d_steps(*l, iterations));
         for (; i < iterations && rc == STENCIL_OK;) {
             const uint32_t n2 = std::min(k, iterations - i);
             rc = launch_tb2d(*l, in, out, int(n2), s);

@@ -88,6 +88,7 @@ bool tb2dp_fits(const stencil_layout& l);  // queries the current device
 int tb2dp_steps(const stencil_problem& p);
 bool tb2d_supports(const stencil_problem& p);
 int tb2d_max_steps(const stencil_problem& p);
+int tb2d_steps(const stencil_layout& l, uint32_t iterations);  // sweeps per launch (queries the device)
 
 // Kernel-family coverage: the z-marching single-sweep family (7-point star
 // and 27-point box, r = 1) and the fused two-step family (same stencils).

@@ -235,6 +235,55 @@ int tb2d_max_steps(const stencil_problem& p) {
     return std::max(1, std::min(k, cap));
 }
 
+namespace {
+// Workgroup slots for the round count: one per CU.  The occupancy API allows
+// two strip workgroups per CU, but measured rounds behave as one per CU (C1
+// fp64: 240 tiles 658 Gcell/s, 260 tiles 571), so the CU count it is.
+int strip_slots() {
+    static int slots = -1;
+    if (slots < 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            slots = 0;
+        else
+            slots = cus;
+    }
+    return slots;
+}
+}  // namespace
+
+// Sweeps per launch in stencil_iterate: among K = 8/r .. 16/r whose tiles take
+// no more rounds of one-per-CU workgroups than K = 8/r, the fewest launches
+// for `iterations`, then the fewest tiles -- more sweeps per launch at no
+// extra round (C1 1024^2 fp64: K = 10, 240 tiles on 256 CUs, 658 vs 610
+// Gcell/s; K = 12 needs 260 tiles, a second round, 571; tools/tb2ds_ab.sh,
+// tools/tb2d_kauto_ab.sh).  STENCIL_TB2D_K / _CFG and r > 2 keep
+// tb2d_max_steps.
+int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
+    const stencil_problem& p = l.prob;
+    const int base = tb2d_max_steps(p);
+    const char* e = std::getenv("STENCIL_TB2D_K");
+    if ((e && *e) || p.radius > 2 || tenv_int("STENCIL_TB2D_CFG", 0)) return base;
+    const int slots = strip_slots();
+    (void)hipGetLastError();
+    if (slots <= 0) return base;
+    auto tiles = [&](int k) -> int64_t {
+        const int64_t h = int64_t(k) * p.radius, tx = 128 - 2 * h, ty = 64 - 2 * h;
+        if (tx < 4 || ty < 4) return INT64_MAX / 2;
+        return (p.nx + tx - 1) / tx * ((p.ny + ty - 1) / ty);
+    };
+    auto rounds = [&](int k) { return (tiles(k) + slots - 1) / slots; };
+    auto launches = [&](int k) { return (int64_t(iterations) + k - 1) / k; };
+    const int64_t r0 = rounds(base);
+    int best = base;
+    for (int k = base + 1; k <= 16 / p.radius; ++k) {
+        if (rounds(k) > r0) continue;
+        if (launches(k) < launches(best) || (launches(k) == launches(best) && tiles(k) < tiles(best))) best = k;
+    }
+    return best;
+}
+
 int launch_tb2d(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
     if (!tb2d_supports(l.prob)) return set_error(STENCIL_EUNSUPPORTED, "tb2d: 2D star r<=4 only");
     const bool dma = l.prob.order == STENCIL_ORDER_DMA;
