@@ -18,6 +18,11 @@ Per round, on each rank (overlap=True):
   chain:    round r+1's interior waits for round r's boundary launches, its
             boundary launches for round r's interior and the received halos
             (events between the two streams; see _round).
+On GPUs with the 7-point star's K-step kernel (the default), a round is
+instead ONE launch over the whole slab (_round_signal): its first z-chunk
+marches up and its last one down, so both K-plane faces are stored first and
+counted in device counters; the exchange stream waits for the counts and sends
+the faces while the launch finishes the interior.
 A round is one sweep (halo depth r), or -- when the backend has a fused
 multi-step kernel and K-deep halos -- K sweeps in one launch per plane range
 (temporal blocking across GPUs: the exchange of K planes every K sweeps, the
