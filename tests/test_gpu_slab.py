@@ -232,11 +232,11 @@ def test_face_signal_counts_completed_faces(gpu, dtype, steps):
     fs.close()
 
 
-def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=True):
+def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=True, dtype="fp64"):
     from stencil_amd.slab import SlabInfo, SlabJacobi
-    spec = StencilSpec(dims=3, dtype="fp64")
+    spec = StencilSpec(dims=3, dtype=dtype)
     fuse = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
-    spec = StencilSpec(dims=3, dtype="fp64", halo=max(2, fuse))
+    spec = StencilSpec(dims=3, dtype=dtype, halo=max(2, fuse))
     e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
     SlabJacobi.use_signal = signalled
     default_fs = SlabJacobi.use_face_signal
@@ -248,6 +248,7 @@ def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=Tru
         SlabJacobi.use_face_signal = default_fs
     assert slab.signalled == signalled
     assert (slab._fsig is not None) == (signalled and face_signal)
+    assert slab.k == fuse
     slab.init("random", 5, plane_elems=nx * ny)
     slab.run(it)
     assert slab.signal_timeouts() == 0
@@ -267,6 +268,24 @@ def test_signalled_rounds_match_boundary_launches(gpu, shape3, it, face_signal):
     want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False)
     got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, face_signal)
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("steps", ["3", "4", "5"])
+@pytest.mark.parametrize("extra,it", [(0, 8), (1, 17), (3, 9), (4, 11), (30, 20)])
+def test_signalled_rounds_every_k(gpu, monkeypatch, dtype, steps, extra, it):
+    """Face-signalled rounds for K = 3, 4, 5 in fp32 and fp64, on slabs from
+    the minimum 2K planes (the launch's chunks shrink to >= K planes each) to
+    several chunks, with a remainder of iterations after the K-rounds --
+    bitwise the boundary + interior rounds."""
+    from stencil_amd.slab import LoopbackExchanger
+    monkeypatch.setenv("STENCIL_TK_STEPS", steps)
+    nz = 2 * int(steps) + extra  # 2K planes: the smallest signalled slab
+    nx, ny = 67, 29
+    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype)
+    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, False, dtype=dtype)
+    ib = torch.int64 if dtype == "fp64" else torch.int32
+    assert torch.equal(got.view(ib), want.view(ib)), (nz, it)
 
 
 def test_signalled_rounds_over_rccl(gpu):
