@@ -186,12 +186,17 @@ int launch_shape(const stencil_layout& l, const void* in, void* out, int steps, 
         case 92808: return launch_tbs<T, ORDER, R, 2, 8, 8>(l, in, out, steps, s);
         case 92816: return launch_tbs<T, ORDER, R, 2, 8, 16>(l, in, out, steps, s);
         case 92408: return launch_tbs<T, ORDER, R, 2, 4, 8>(l, in, out, steps, s);
+        case 92416: return launch_tbs<T, ORDER, R, 2, 4, 16>(l, in, out, steps, s);
+        case 92216: return launch_tbs<T, ORDER, R, 2, 2, 16>(l, in, out, steps, s);
         case 94808: return launch_tbs<T, ORDER, R, 4, 8, 8>(l, in, out, steps, s);
         case 92608: return launch_tbs<T, ORDER, R, 2, 6, 8>(l, in, out, steps, s);
         case 0:
-            // default for r <= 2: 128 x 64 regions (2 cells per lane, 8 rows x 8
-            // waves); 1024^2, K = 8: fp64 559 vs 393 Gcell/s for the LDS kernel,
-            // fp32 709 vs 520 (tools/tb2d_ab.sh)
+            // default for r <= 2: 128 x 64 regions, 2 cells per lane (1024^2,
+            // K = 8: fp64 559 vs 393 Gcell/s for the LDS kernel, fp32 709 vs
+            // 520; tools/tb2d_ab.sh); fp64 as 16 waves x 4 rows (C1, K = 10: 694
+            // vs 652 Gcell/s for 8 x 8 -- more waves hide the per-sweep
+            // barrier; tools/tb2ds_shape_ab.sh), fp32 as 8 x 8
+            if constexpr (sizeof(T) == 8) return launch_tbs<T, ORDER, R, 2, 4, 16>(l, in, out, steps, s);
             return launch_tbs<T, ORDER, R, 2, 8, 8>(l, in, out, steps, s);
         default: break;
         }
@@ -264,7 +269,8 @@ int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
     const stencil_problem& p = l.prob;
     const int base = tb2d_max_steps(p);
     const char* e = std::getenv("STENCIL_TB2D_K");
-    if ((e && *e) || p.radius > 2 || tenv_int("STENCIL_TB2D_CFG", 0)) return base;
+    const int cfg = tenv_int("STENCIL_TB2D_CFG", 0);
+    if ((e && *e) || p.radius > 2 || (cfg != 0 && cfg != 92808 && cfg != 92416)) return base;  // 128 x 64 only
     const int slots = strip_slots();
     (void)hipGetLastError();
     if (slots <= 0) return base;
