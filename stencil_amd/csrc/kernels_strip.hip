@@ -65,6 +65,23 @@ __device__ __forceinline__ double sdpp(double v) {
 }
 constexpr int kSShr1 = 0x138, kSShl1 = 0x130;  // wave_shr:1 / wave_shl:1
 
+// The plane loop unrolled N steps (compile-time step index), and the tail of
+// fewer than N steps.
+template <int I, int N, typename F>
+__device__ __forceinline__ void unroll_steps(F& f, int p) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{}, p + I);
+        unroll_steps<I + 1, N>(f, p);
+    }
+}
+template <int I, int N, typename F>
+__device__ __forceinline__ void tail_steps(F& f, int p, int plast) {
+    if constexpr (I < N) {
+        if (p + I <= plast) f(std::integral_constant<int, I>{}, p + I);
+        tail_steps<I + 1, N>(f, p, plast);
+    }
+}
+
 template <typename T, int V, int RY, int NW, int K, bool DB>
 struct StripTile {
     static constexpr int XR = (K + V - 1) / V;  // ring vectors per x side
@@ -90,7 +107,9 @@ struct StripTile {
 // run on across launches: every tiles_x*tiles_y-th add) also adds 1 to
 // *fsig, so the command processor can gate the exchange stream on it
 // (hipStreamWaitValue64) with no wait kernel resident during the launch.
-template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false>
+// NS: input planes in registers -- in(p-2) .. in(p+NS-3): loads are issued
+// NS-2 planes ahead (4: two planes).
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
@@ -190,11 +209,13 @@ __global__ void __launch_bounds__(64 * NW)
         for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
     };
 
+    static_assert(NS >= 4, "the input ring holds in(p-2) .. in(p+1) at least");
+    constexpr int LCM = NS % 2 == 0 ? NS : 2 * NS;  // steps until ring slot and H parity repeat
     const int p0 = za - K;
-    VT vin[4][RY];                  // slot (q - p0) & 3 holds in(q)
+    VT vin[NS][RY];                 // slot (q - p0) % NS holds in(q)
     VT H[K > 1 ? K - 1 : 1][2][RY]; // H[s-1][(q - p0) & 1] holds t_s(q), s < K
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NS; ++i)
 #pragma unroll
         for (int k = 0; k < RY; ++k) vin[i][k] = VT{};
 #pragma unroll
@@ -203,12 +224,12 @@ __global__ void __launch_bounds__(64 * NW)
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int k = 0; k < RY; ++k) H[s][b][k] = VT{};
-    load_plane(vin[0], p0);
-    load_plane(vin[1], p0 + 1);
+#pragma unroll
+    for (int i = 0; i < NS - 2; ++i) load_plane(vin[i], p0 + i);
 
 
     auto step = [&](auto S_, int p) {
-        constexpr int S = decltype(S_)::value;  // (p - p0) & 3
+        constexpr int S = decltype(S_)::value;  // (p - p0) % LCM
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
         constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
         __syncthreads();  // boundary rows of step p-1 are visible
@@ -239,11 +260,11 @@ __global__ void __launch_bounds__(64 * NW)
                 // t_{s-1} planes p-s (centre), p-s-1 (z-), p-s+1 (z+)
                 VT c, zm, zp, up, dn;
                 if constexpr (s == 1) {
-                    c = vin[(S + 3) & 3][k];
-                    zm = vin[(S + 2) & 3][k];
-                    zp = vin[S][k];
-                    up = k == 0 ? STRIP_ABOVE(0) : vin[(S + 3) & 3][k == 0 ? 0 : k - 1];
-                    dn = k == RY - 1 ? STRIP_BELOW(0) : vin[(S + 3) & 3][k == RY - 1 ? 0 : k + 1];
+                    c = vin[(S + NS - 1) % NS][k];
+                    zm = vin[(S + NS - 2) % NS][k];
+                    zp = vin[S % NS][k];
+                    up = k == 0 ? STRIP_ABOVE(0) : vin[(S + NS - 1) % NS][k == 0 ? 0 : k - 1];
+                    dn = k == RY - 1 ? STRIP_BELOW(0) : vin[(S + NS - 1) % NS][k == RY - 1 ? 0 : k + 1];
                 } else {
                     c = H[s - 2][(S - s + 4) & 1][k];
                     zm = H[s - 2][(S - s + 5) & 1][k];
@@ -290,8 +311,8 @@ __global__ void __launch_bounds__(64 * NW)
         }
         // boundary rows for step p+1: stage 1's centre is in(p), stage s's is t_{s-1}(p-s+1)
         if constexpr (!DB) __syncthreads();  // single buffer: every read of it is done
-        *reinterpret_cast<VT*>(&L[P][0][w][0][xl]) = vin[S][0];
-        *reinterpret_cast<VT*>(&L[P][0][w][1][xl]) = vin[S][RY - 1];
+        *reinterpret_cast<VT*>(&L[P][0][w][0][xl]) = vin[S % NS][0];
+        *reinterpret_cast<VT*>(&L[P][0][w][1][xl]) = vin[S % NS][RY - 1];
 #pragma unroll
         for (int s = 2; s <= K; ++s) {  // t_{s-1}(p-s+1), now in H
             *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = H[s - 2][(S - s + 5) & 1][0];
@@ -328,20 +349,13 @@ __global__ void __launch_bounds__(64 * NW)
                 }
             }
         }
-        if constexpr (DIAG != 1) load_plane(vin[(S + 2) & 3], p + 2);  // slot of in(p-2), consumed above
+        if constexpr (DIAG != 1) load_plane(vin[(S + NS - 2) % NS], p + NS - 2);  // slot of in(p-2), consumed above
     };
 
     const int plast = zb + K - 1;
     int p = p0;
-    for (; p + 3 <= plast; p += 4) {
-        step(std::integral_constant<int, 0>{}, p);
-        step(std::integral_constant<int, 1>{}, p + 1);
-        step(std::integral_constant<int, 2>{}, p + 2);
-        step(std::integral_constant<int, 3>{}, p + 3);
-    }
-    if (p <= plast) step(std::integral_constant<int, 0>{}, p);
-    if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
-    if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
+    for (; p + LCM - 1 <= plast; p += LCM) unroll_steps<0, LCM>(step, p);
+    tail_steps<0, LCM - 1>(step, p, plast);
     };  // segment
     while (lo < hi) {
         if constexpr (SIG) {
@@ -358,7 +372,7 @@ int senv_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false>
+template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
@@ -369,7 +383,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG>;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS>;
     const int64_t tiles = gx * gy;
     int zc = senv_int("STENCIL_TK_ZCHUNK", 0);
     int64_t nb = 0;
@@ -494,6 +508,10 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 10808: return launch_st<double, 1, 8, 8, 4>(l, in, out, begin, end, s);
             case 10608: return launch_st<double, 1, 6, 8, 4>(l, in, out, begin, end, s);
             case 404: return launch_st<double, 2, 4, 8, 4>(l, in, out, begin, end, s);
+            case 510708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
+            case 510608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
+            case 610608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
+            case 610508: return launch_st<double, 1, 5, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
             default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
             }
         }
