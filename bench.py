@@ -294,6 +294,13 @@ def main():
                                   "events around the interior launches of extra rounds after the timed region"),
             },
         }
+        traffic = out["roofline"]["traffic"]
+        if traffic and launch_ms > 0:
+            # the PMC-measured bytes of one launch over its live mean duration:
+            # the HBM-side rate (the algorithmic `achieved` counts 16 B per
+            # update, which K fused sweeps per launch take far past the peak)
+            out["roofline"]["traffic_GBps"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
+            out["roofline"]["traffic_frac"] = round(out["roofline"]["traffic_GBps"] / HBM_PEAK_GBPS, 4)
         try:
             out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
         except Exception as exc:  # calibration only
