@@ -527,6 +527,11 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
         if (kernel) *kernel = STENCIL_KERNEL_PERSISTENT;
         return STENCIL_OK;
     }
+    if (iterate_tb2d(l->prob) && tb2d1_fits(*l)) {
+        if (launches) *launches = iterations ? 1 : 0;
+        if (kernel) *kernel = STENCIL_KERNEL_TEMPORAL2;
+        return STENCIL_OK;
+    }
     if (iterate_tb2d(l->prob)) {
         const int64_t k = tb2d_steps(*l, iterations);
         if (launches) *launches = (int64_t(iterations) + k - 1) / k;
@@ -573,6 +578,15 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
         } else if (rc == STENCIL_EUNSUPPORTED) {
             rc = STENCIL_OK;  // tiles do not fit at once: K-step launches below
             clear_error();
+        }
+    }
+    if (iterate_tb2d(l->prob) && rc == STENCIL_OK && i < iterations && tb2d1_fits(*l)) {
+        // the whole grid in one workgroup's LDS: every sweep in one launch,
+        // the result where the per-sweep ping-pong would leave it
+        rc = launch_tb2d1(*l, in, (iterations - i) % 2 ? out : in, iterations - i, s);
+        if (rc == STENCIL_OK) {
+            if ((iterations - i) % 2) std::swap(in, out);
+            i = iterations;
         }
     }
     if (iterate_tb2d(l->prob) && rc == STENCIL_OK) {

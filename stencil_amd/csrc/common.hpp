@@ -89,6 +89,9 @@ int tb2dp_steps(const stencil_problem& p);
 bool tb2d_supports(const stencil_problem& p);
 int tb2d_max_steps(const stencil_problem& p);
 int tb2d_steps(const stencil_layout& l, uint32_t iterations);  // sweeps per launch (queries the device)
+// a 2D grid small enough for one workgroup's LDS: the whole job in one launch
+bool tb2d1_fits(const stencil_layout& l);
+int launch_tb2d1(const stencil_layout& l, const void* in, void* out, uint32_t iterations, hipStream_t s);
 
 // Kernel-family coverage: the z-marching single-sweep family (7-point star
 // and 27-point box, r = 1) and the fused two-step family (same stencils).

@@ -147,6 +147,90 @@ int launch_tb(const stencil_layout& l, const void* in, void* out, int steps, hip
     return STENCIL_OK;
 }
 
+// The whole grid (ghost ring included) in ONE workgroup's LDS, two images:
+// every sweep of the job in one launch, one workgroup barrier per sweep and
+// no global traffic between the first load and the last store.  For the
+// small grids the reference's own tests use (n = 32, 64): a K-step launch
+// costs ~1.7 us of boundary per launch and its 8-wave strips ~1.5 us per
+// sweep there.  Each thread owns up to k1MaxCells cells (offsets kept in
+// registers).  Measured per sweep (tools/tb2d1_ab.sh): 32^2 0.5 vs 0.8-0.9
+// us, 64^2 0.7 vs 0.8-1.0; at 96^2 (9 cells per thread) 1.1-1.2 vs 0.8-1.0,
+// so only grids of <= 5 cells per thread take this path.
+constexpr int k1Threads = 1024;
+constexpr int k1MaxCells = 5;  // per thread: grids up to 5120 cells
+template <typename T, int ORDER, int R>
+__global__ void __launch_bounds__(k1Threads)
+    tb2d1(const T* __restrict__ in, T* __restrict__ out, Geom g, int iterations, T avg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem1[];
+    T* img0 = reinterpret_cast<T*>(smem1);
+    const int nx = int(g.nx), ny = int(g.ny);
+    const int S = nx + 2 * R;  // LDS row stride
+    const int Hh = ny + 2 * R;
+    T* img1 = img0 + S * Hh;
+    const int tid = int(threadIdx.x);
+    const T* __restrict__ src = in + g.origin;
+    for (int i = tid; i < S * Hh; i += k1Threads) {
+        const int y = i / S - R, x = i % S - R;
+        const T v = src[int64_t(y) * g.row + x];
+        img0[i] = v;
+        img1[i] = v;
+    }
+    int off[k1MaxCells];  // LDS index of this thread's cells (interior only)
+    int nc = 0;
+#pragma unroll
+    for (int c = 0; c < k1MaxCells; ++c) {
+        const int i = tid + c * k1Threads;
+        off[c] = i < nx * ny ? (i / nx + R) * S + i % nx + R : 0;
+        nc += i < nx * ny ? 1 : 0;
+    }
+    __syncthreads();
+    for (int it = 0; it < iterations; ++it) {
+        const T* a = (it & 1) ? img1 : img0;
+        T* b = (it & 1) ? img0 : img1;
+#pragma unroll
+        for (int c = 0; c < k1MaxCells; ++c)
+            if (c < nc) b[off[c]] = cell2d<T, ORDER, R>(a + off[c], S, avg);
+        __syncthreads();
+    }
+    const T* fin = (iterations & 1) ? img1 : img0;
+    T* __restrict__ dst = out + g.origin;
+#pragma unroll
+    for (int c = 0; c < k1MaxCells; ++c) {
+        if (c < nc) {
+            const int i = tid + c * k1Threads;
+            dst[int64_t(i / nx) * g.row + i % nx] = fin[off[c]];
+        }
+    }
+}
+
+template <typename T, int ORDER, int R>
+int launch_tb1(const stencil_layout& l, const void* in, void* out, uint32_t iterations, hipStream_t s) {
+    const Geom g = geom_of(l);
+    const size_t lds = size_t(2) * size_t(g.nx + 2 * R) * size_t(g.ny + 2 * R) * sizeof(T);
+    auto kern = tb2d1<T, ORDER, R>;
+    static bool attr = false;
+    if (!attr) {
+        STENCIL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(k1Threads), lds, s, static_cast<const T*>(in), static_cast<T*>(out), g,
+                       int(iterations), avg_weight<T>(l.prob));
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
+}
+
+template <typename T, int ORDER>
+int launch_tb1_r(const stencil_layout& l, const void* in, void* out, uint32_t iterations, hipStream_t s) {
+    switch (l.prob.radius) {
+    case 1: return launch_tb1<T, ORDER, 1>(l, in, out, iterations, s);
+    case 2: return launch_tb1<T, ORDER, 2>(l, in, out, iterations, s);
+    case 3: return launch_tb1<T, ORDER, 3>(l, in, out, iterations, s);
+    case 4: return launch_tb1<T, ORDER, 4>(l, in, out, iterations, s);
+    default: return set_error(STENCIL_EUNSUPPORTED, "tb2d1: radius > 4");
+    }
+}
+
 // Strip variant (R <= V): strip2d.hpp.
 template <typename T, int ORDER, int R, int V, int RY, int NW>
 __global__ void __launch_bounds__(64 * NW)
@@ -288,6 +372,28 @@ int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
         if (launches(k) < launches(best) || (launches(k) == launches(best) && tiles(k) < tiles(best))) best = k;
     }
     return best;
+}
+
+bool tb2d1_fits(const stencil_layout& l) {
+    const stencil_problem& p = l.prob;
+    if (!tb2d_supports(p) || p.nx <= 0 || p.ny <= 0) return false;
+    const char* e = std::getenv("STENCIL_TB2D_SINGLE");
+    if (e && *e == '0') return false;
+    const int64_t esz = p.dtype == STENCIL_F32 ? 4 : 8;
+    const int64_t lds = 2 * (p.nx + 2 * p.radius) * (p.ny + 2 * p.radius) * esz;
+    return p.nx * p.ny <= int64_t(k1Threads) * k1MaxCells && lds <= 160 * 1024;
+}
+
+// `iterations` sweeps of a grid that fits one workgroup (tb2d1_fits), from
+// `in`; the result lands in `out`.
+int launch_tb2d1(const stencil_layout& l, const void* in, void* out, uint32_t iterations, hipStream_t s) {
+    if (!tb2d1_fits(l)) return set_error(STENCIL_EUNSUPPORTED, "tb2d1: grid does not fit one workgroup");
+    const bool dma = l.prob.order == STENCIL_ORDER_DMA;
+    if (l.prob.dtype == STENCIL_F32)
+        return dma ? launch_tb1_r<float, STENCIL_ORDER_DMA>(l, in, out, iterations, s)
+                   : launch_tb1_r<float, STENCIL_ORDER_NAIVE>(l, in, out, iterations, s);
+    return dma ? launch_tb1_r<double, STENCIL_ORDER_DMA>(l, in, out, iterations, s)
+               : launch_tb1_r<double, STENCIL_ORDER_NAIVE>(l, in, out, iterations, s);
 }
 
 int launch_tb2d(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {

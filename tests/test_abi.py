@@ -110,7 +110,11 @@ def test_plan_counts_launches(monkeypatch):
     lay2 = _lib.make_layout(_lib.make_problem(dims=2, nx=64, ny=64))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay2), 100, ctypes.byref(launches), ctypes.byref(kernel)) == 0
-    assert launches.value == 13 and kernel.value == _lib.KERNEL_TEMPORAL2  # 2D: 8 sweeps per launch in LDS
+    assert launches.value == 1 and kernel.value == _lib.KERNEL_TEMPORAL2  # 2D, fits one workgroup: one launch
+    lay2 = _lib.make_layout(_lib.make_problem(dims=2, nx=300, ny=300))
+    assert lib.stencil_plan(ctypes.byref(lay2), 100, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    # 2D: 8 sweeps per launch without a GPU to query; up to 16 where one round of tiles fits the CUs
+    assert launches.value in {-(-100 // k) for k in range(8, 17)} and kernel.value == _lib.KERNEL_TEMPORAL2
     lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0

@@ -87,6 +87,7 @@ def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
     kernel and of the register-strip kernel (cfg 9xxxx, r <= 2), ragged grids
     spanning several tiles, iteration counts that leave a partial last launch."""
     monkeypatch.setenv("STENCIL_TB2D_K", k)
+    monkeypatch.setenv("STENCIL_TB2D_SINGLE", "0")  # the K-step launches even where one workgroup fits
     if cfg != "default":
         monkeypatch.setenv("STENCIL_TB2D_CFG", cfg)
     strip = cfg.startswith("9") and r <= 2
@@ -100,6 +101,25 @@ def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
         want = ob.run(p, it, "random", 8 + r)
         _, got = gpu_run(gpu, 2, dtype, "star", r, order, "temporal2", nx, ny, 1, it, "random", 8 + r)
         assert same_bits(got, want), (nx, ny, it)
+
+
+@pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma"), (3, "dma"), (4, "naive")])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_2d_single_workgroup(gpu, r, order, dtype):
+    """Grids that fit one workgroup's LDS run every sweep in one launch
+    (kernels_tb2d.hip tb2d1): odd and even iteration counts (the result lands
+    where the ping-pong would leave it), ragged, one-cell and one-row grids,
+    the largest grids that take the path and the first that do not."""
+    esz = 4 if dtype == "fp32" else 8
+    for nx, ny, it in ((32, 32, 3), (64, 64, 100), (1, 1, 2), (77, 13, 7), (5120, 1, 5), (80, 64, 5), (71, 72, 4),
+                       (40, 40, 0)):
+        p = ob.problem(2, dtype, "star", r, order, nx, ny)
+        want = ob.run(p, it, "random", 3 + r)
+        e, got = gpu_run(gpu, 2, dtype, "star", r, order, "auto", nx, ny, 1, it, "random", 3 + r)
+        assert same_bits(got, want), (nx, ny, it)
+        single = nx * ny <= 5120 and 2 * (nx + 2 * r) * (ny + 2 * r) * esz <= 160 * 1024
+        if it and single:
+            assert e.plan(it)[0] == 1, (nx, ny, it)
 
 
 @pytest.mark.parametrize("k", ["1", "3", "8", "12"])
