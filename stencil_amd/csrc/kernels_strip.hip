@@ -37,8 +37,12 @@
 // kernels_temporalk.hip; intermediate planes keep ghost cells at their input
 // value; slab-halo planes (HALO_LO/HI) are advanced.  Bitwise equal to K
 // plain sweeps (tests/test_gpu_parity.py).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <tuple>
+#include <vector>
 
 #include "common.hpp"
 
@@ -113,7 +117,7 @@ template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool 
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -130,7 +134,12 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t tiles = int64_t(tiles_x) * tiles_y;
     int64_t lo, hi;
     bool rev = false;  // this workgroup's chunk marches down (SIG: the last chunk)
-    if (zchunk > 0) {
+    if (sched) {
+        // packed schedule (STENCIL_TK_PACK): {tile, first plane, planes} per workgroup
+        const int* e = sched + 3 * int64_t(blockIdx.x);
+        lo = int64_t(e[0]) * nzr + e[1];
+        hi = lo + e[2];
+    } else if (zchunk > 0) {
         const int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
         lo = t * nzr + c * zchunk;
         hi = lo + (zchunk < nzr - c * zchunk ? zchunk : nzr - c * zchunk);
@@ -372,6 +381,86 @@ int senv_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
+// Makespan (in plane steps) of workgroups of the given plane counts on
+// `slots` one-workgroup CU slots: workgroup i goes to XCD i % 8 (the
+// dispatcher's round robin), and inside an XCD to the slot that frees first
+// (in-order dispatch); a chunk of n planes costs n + 2K steps (pipeline fill).
+int64_t simulate_makespan(const std::vector<int>& len, int K, int slots) {
+    constexpr int kXcd = 8;
+    const int per = std::max(1, slots / kXcd);
+    std::vector<std::vector<int64_t>> free_at(kXcd, std::vector<int64_t>(per, 0));
+    int64_t span = 0;
+    for (size_t i = 0; i < len.size(); ++i) {
+        auto& f = free_at[i % kXcd];
+        auto it = std::min_element(f.begin(), f.end());
+        *it += len[i] + 2 * K;
+        span = std::max(span, *it);
+    }
+    return span;
+}
+
+// STENCIL_TK_PACK (default 1; 0 = equal chunks): chunks of Lc planes per tile (the last one
+// shorter), longest first -- every tile's full chunks start in z lock-step,
+// the short remainders fill the CUs the full chunks leave idle.  Lc is the
+// one with the shortest simulated makespan; used only when it beats the
+// equal-chunk grid (zc planes per chunk) by 2 %.  The table is built once per
+// shape and kept for the process.
+int packed_schedule(int64_t tiles, int64_t nz, int K, int slots, int zc, const int** sched, int64_t* nb) {
+    // Only grids of few tiles: with more than 2 tiles per slot the equal
+    // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
+    // Gcell/s), and the search would cost host time at the first launch.
+    if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
+    static std::map<std::tuple<int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
+    const auto key = std::make_tuple(tiles, nz, K, slots);
+    auto hit = cache.find(key);
+    if (hit == cache.end()) {
+        auto build = [&](int64_t lc, std::vector<int>& tab) {
+            struct Item { int len, c, t, z; };
+            std::vector<Item> items;
+            for (int64_t t = 0; t < tiles; ++t)
+                for (int64_t z = 0, c = 0; z < nz; z += lc, ++c)
+                    items.push_back({int(std::min<int64_t>(lc, nz - z)), int(c), int(t), int(z)});
+            std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+                return a.len != b.len ? a.len > b.len : (a.c != b.c ? a.c < b.c : a.t < b.t);
+            });
+            std::vector<int> len;
+            tab.clear();
+            for (const Item& it : items) {
+                len.push_back(it.len);
+                tab.insert(tab.end(), {it.t, it.z, it.len});
+            }
+            return simulate_makespan(len, K, slots);
+        };
+        std::vector<int> tab, best_tab;
+        const int64_t base = build(zc, tab);
+        int64_t best = base;
+        for (int64_t lc = std::max<int64_t>(2 * K, nz / 16); lc <= nz; lc += std::max<int64_t>(1, nz / 256)) {
+            const int64_t m = build(lc, tab);
+            if (m < best) best = m, best_tab = tab;
+        }
+        int* d = nullptr;
+        int64_t n = 0;
+        if (!best_tab.empty() && best * 50 < base * 49) {
+            if (hipMalloc(&d, best_tab.size() * sizeof(int)) != hipSuccess ||
+                hipMemcpy(d, best_tab.data(), best_tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+                // a pageable H2D copy may return before its DMA lands, and the
+                // launch goes to another stream: wait for it (once per shape)
+                hipDeviceSynchronize() != hipSuccess)
+                return set_error(STENCIL_EHIP, "packed schedule upload failed");
+            n = int64_t(best_tab.size() / 3);
+        }
+        if (senv_int("STENCIL_TK_VERBOSE", 0))
+            std::fprintf(stderr, "tkstrip pack: equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n",
+                         (long long)base, (long long)best, (long long)n, d ? "" : " -- not used");
+        hit = cache.emplace(key, std::make_pair(d, n)).first;
+    }
+    if (hit->second.first) {
+        *sched = hit->second.first;
+        *nb = hit->second.second;
+    }
+    return STENCIL_OK;
+}
+
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
@@ -446,6 +535,20 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         nb = tiles * nch;
         if (nsig) *nsig = int(tiles);
     }
+    const int* sched = nullptr;
+    // default: the packed longest-first schedule when it beats equal chunks
+    // (512^3 fp64 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a
+    // multi-GPU job, whose one-round grid above is deliberate
+    if (!SIG && senv_int("STENCIL_TK_PACK", 1) && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
+        !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
+            return set_error(STENCIL_EHIP, "occupancy query failed");
+        const int rc = packed_schedule(gx * gy, nz, K, std::max(1, cus * std::max(1, per_cu)), zc, &sched, &nb);
+        if (rc != STENCIL_OK) return rc;
+    }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
     if (senv_int("STENCIL_TK_VERBOSE", 0)) {
         int per_cu = 0;
@@ -459,7 +562,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
                          (long long)l.zghost);
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       avg_weight<T>(l.prob), sig, fsig);
+                       avg_weight<T>(l.prob), sig, fsig, sched);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
