@@ -134,8 +134,9 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t tiles = int64_t(tiles_x) * tiles_y;
     int64_t lo, hi;
     bool rev = false;  // this workgroup's chunk marches down (SIG: the last chunk)
-    if (sched) {
-        // packed schedule (STENCIL_TK_PACK): {tile, first plane, planes} per workgroup
+    if (!SIG && sched) {
+        // packed schedule (STENCIL_TK_PACK, never on the face-signalled
+        // launches, whose code stays as it was): {tile, first plane, planes}
         const int* e = sched + 3 * int64_t(blockIdx.x);
         lo = int64_t(e[0]) * nzr + e[1];
         hi = lo + e[2];
