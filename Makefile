@@ -35,6 +35,7 @@ $(CLI): $(HOST_SRCS) $(HOST_HDRS) $(LIB) include/stencil_hip.h
 
 oracle:
 	$(MAKE) -C oracle
+	bash oracle/ref/build.sh
 
 clean:
 	rm -rf build $(LIB)

@@ -50,7 +50,30 @@ PRESETS = {
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
     "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
                desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, 2-step temporal blocking"),
+    # north_star's 4096^3 fp64 needs 2 x 550 GB; its largest single-GPU
+    # proxy is 2048^3 fp64: 2 x 70 GB with ghosts and padding
+    "NS": dict(dtype="fp64", shape="star", grid=(2048, 2048, 2048), min_gpus=1,
+               desc="north-star proxy: 3D 7-point fp64 Jacobi, 2048^3 (4096^3 does not fit one GPU)"),
 }
+
+# Kernel family (bench name) -> the sources that define it, hashed into the
+# traffic table so a PMC figure measured on older kernel code is not reported.
+KERNEL_SOURCES = {
+    "temporalk": ("stencil_amd/csrc/kernels_strip.hip", "stencil_amd/csrc/kernels_temporalk.hip"),
+    "temporal2": ("stencil_amd/csrc/kernels_temporal.hip",),
+    "zmarch": ("stencil_amd/csrc/kernels_zmarch.hip",),
+    "direct": ("stencil_amd/csrc/kernels_direct.hip",),
+    "boxk": ("stencil_amd/csrc/kernels_boxk.hip",),
+}
+
+
+def kernel_source_sha(kname: str):
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES.get(kname, ()):
+        with open(os.path.join(HERE, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16] if kname in KERNEL_SOURCES else None
 
 
 def parse():
@@ -107,13 +130,19 @@ def cpu_baseline(n: int, budget_s: float, threads: int = 1, dtype: str = "fp64",
 
 
 def load_traffic(workload_key: str, kernel_name: str):
+    """PMC bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, tools/summarize_profile.py)
+    and the table entry; the bytes are None when the entry was measured on
+    other kernel sources than the ones this tree builds (stale)."""
     path = os.path.join(HERE, "profiles", "traffic.json")
     try:
         data = json.load(open(path))
     except (OSError, ValueError):
-        return None
+        return None, None
     ent = data.get(workload_key, {}).get(kernel_name)
-    return ent.get("hbm_bytes_per_launch") if ent else None
+    if not ent:
+        return None, None
+    fresh = ent.get("kernel_source_sha") == kernel_source_sha(kernel_name)
+    return (ent.get("hbm_bytes_per_launch") if fresh else None), dict(ent, fresh=fresh)
 
 
 def main():
@@ -182,6 +211,8 @@ def main():
     slab.init("reference")
     kernel_id = eng.plan(12)[1]
     kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
+    if spec.shape == "box" and kname in ("temporal2", "temporalk"):
+        kname = "boxk"  # the box's fused family (kernels_boxk.hip)
     multi = world > 1 or loop  # the slab round structure (exchange + two streams)
     sweeps_per_launch = eng.fuse_steps if not multi else slab.launches_per_round()
 
@@ -230,13 +261,19 @@ def main():
     total_updates = float(gnx) * gny * gnz * args.steps
     gcell = total_updates / elapsed / 1e9
     bytes_per_update = 2 * spec.elem_bytes
-    # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
+    # Roofline of the dominant kernel.  One launch advances its cells by
+    # `sweeps_per_launch` fused sweeps; its compulsory HBM traffic is one read
+    # plus one write of those cells (2 * sizeof(T) per cell, whatever K is):
+    # `achieved` = compulsory bytes / mean launch time, a true fraction of the
+    # HBM peak.  The per-sweep algorithmic figure of SURVEY §8(d) (2 * sizeof(T)
+    # per cell-UPDATE, K per cell per launch) is `effective_GBps`.
     edge = slab.depth if slab.fused else max(1, slab.depth)
     # the timed launch: the whole slab (single-GPU job, or face-signalled
     # slab rounds) or the interior between the two boundary launches
     whole = not multi or slab.signalled
     cells_per_launch = cells_per_gpu if whole else cells_per_gpu * (count - 2 * edge) / count
-    alg_bytes_launch = cells_per_launch * bytes_per_update * sweeps_per_launch
+    compulsory_bytes_launch = cells_per_launch * bytes_per_update
+    alg_bytes_launch = compulsory_bytes_launch * sweeps_per_launch
     if not multi:
         # device time per `sweeps_per_launch` sweeps, charged pro rata (with
         # K = 4 a 1000-step job is 250 fused launches; a K that does not divide
@@ -244,10 +281,12 @@ def main():
         launch_ms = kernel_ms_total * sweeps_per_launch / max(1, args.steps)
     else:
         launch_ms = kernel_ms_total / max(1, kernel_launches)
-    achieved = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
+    achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9
+    effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
 
     if rank == 0:
         workload = f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{count}"
+        traffic, traffic_entry = load_traffic(workload, kname)
         desc = pre["desc"].format(n=n)
         out = {
             "metric": METRIC,
@@ -284,7 +323,13 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic(workload, kname),
+                "traffic": traffic,
+                "bytes_basis": "compulsory: one read + one write of the launch's cells (2 x %d B per cell), "
+                               "%d fused sweeps per launch" % (spec.elem_bytes, sweeps_per_launch),
+                "compulsory_bytes_per_launch": compulsory_bytes_launch,
+                "effective_GBps": round(effective, 1),
+                "effective_basis": "SURVEY 8(d) algorithmic: 2 x %d B per cell-update x %d sweeps per launch"
+                                   % (spec.elem_bytes, sweeps_per_launch),
                 "alg_bytes_per_launch": alg_bytes_launch,
                 "mean_launch_ms": round(launch_ms, 5),
                 "launches": kernel_launches,
@@ -294,11 +339,13 @@ def main():
                                   "events around the interior launches of extra rounds after the timed region"),
             },
         }
-        traffic = out["roofline"]["traffic"]
+        if traffic_entry is not None:
+            out["roofline"]["traffic_source"] = {k: traffic_entry.get(k) for k in
+                                                 ("source", "kernel", "kernel_source_sha", "fresh")}
         if traffic and launch_ms > 0:
-            # the PMC-measured bytes of one launch over its live mean duration:
-            # the HBM-side rate (the algorithmic `achieved` counts 16 B per
-            # update, which K fused sweeps per launch take far past the peak)
+            # the PMC-measured bytes of one launch (L2->fabric: HBM plus
+            # Infinity-Cache hits) over its live mean duration; traffic well
+            # above the compulsory bytes = re-reads (tile rings, halos)
             out["roofline"]["traffic_GBps"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
             out["roofline"]["traffic_frac"] = round(out["roofline"]["traffic_GBps"] / HBM_PEAK_GBPS, 4)
         try:

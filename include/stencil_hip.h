@@ -191,6 +191,14 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
 int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
                    int32_t steps, void* stream);
 
+/* Launch geometry of stencil_sweepk's K-step kernel (3D r=1 7-point star,
+ * steps 3..5) on [begin, end), computed as the launch would, without
+ * launching: workgroups, planes per z-chunk (0 = balanced shares) and
+ * whether the packed longest-first chunk schedule is used (it is built and
+ * uploaded on first use).  Queries the current device. */
+int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end, int32_t steps, int64_t* workgroups,
+                            int32_t* zchunk, int32_t* packed);
+
 /* Multi-GPU slabs: stencil_sweepk over [begin, end) (3D 7-point star, steps
  * 3..5) as ONE launch whose workgroups add 1 to counters[0] as soon as the
  * low face planes [begin, begin+steps) are stored and to counters[1] for

@@ -16,13 +16,16 @@
  *   - neighbors_impl::stencil_iterate_dma arithmetic,
  *     src/stencil/slave/stencil_dma.cpp:636-650,700-720    ("dma" order, r > 1)
  *
- * Pinning: the reference cannot be built here (its kernels and stencil.cpp
- * need the Sunway athread.h/crts.h, absent from the image), so there is no
- * oracle/_ref.  The restatement is pinned by the known answers SURVEY.md §8c
- * recorded from the reference itself (fp32 naive == reference
- * DMAStaticUnroll, reference DMA / DMASlavePack hashes); see
- * tests/test_oracle_golden.py.  3D, box shapes and fp64 have no reference
- * semantics ("parity unpinned" -- see DESIGN.md §Oracle).
+ * Pinning: oracle/ref/build.sh compiles the reference's OWN naive loop
+ * (stencil.cpp:77-131) and initial condition (190-207) from /root/reference
+ * with its real headers into oracle/_ref/ref_naive (the lines are piped into
+ * g++; no stand-in header: the athread include, stencil.cpp:2, is outside the
+ * slice).  tests/golden/make_ref_golden.py records its outputs; the 2D naive
+ * restatement here equals them bit for bit in fp32 (and in fp64 against the
+ * same lines with float -> double), C1 included (tests/test_oracle_golden.py).
+ * The reference's CPE kernels (DMA order) need the Sunway athread SDK and are
+ * pinned by the deviation statistics SURVEY.md §8c recorded from its probe.
+ * 3D and box shapes have no reference code ("parity unpinned" -- DESIGN.md §4).
  *
  * Layout: a dense ghost-padded array, x fastest.  Extents with ghosts are
  *   sx = nx + 2r, sy = ny + 2r, sz = (dims == 3 ? nz + 2r : 1).

@@ -10,6 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "common.hpp"
@@ -20,6 +23,8 @@ namespace {
 thread_local int g_last_code = STENCIL_OK;
 thread_local char g_last_msg[512] = "";
 }  // namespace
+
+thread_local LaunchInfo* tl_dry_launch = nullptr;
 
 int set_error(int code, const char* fmt, ...) {
     g_last_code = code;
@@ -33,6 +38,30 @@ int set_error(int code, const char* fmt, ...) {
 void clear_error() {
     g_last_code = STENCIL_OK;
     g_last_msg[0] = '\0';
+}
+
+int resident_slots(const void* kern, int threads, bool one_per_cu, int* slots) {
+    int dev = 0;
+    STENCIL_HIP_CHECK(hipGetDevice(&dev));
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void*, int, bool>, int> cache;
+    const auto key = std::make_tuple(dev, kern, threads, one_per_cu);
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) {
+            *slots = it->second;
+            return STENCIL_OK;
+        }
+    }
+    int cus = 0, per_cu = 1;
+    STENCIL_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (!one_per_cu) STENCIL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0));
+    const int n = std::max(1, cus * std::max(1, per_cu));
+    std::lock_guard<std::mutex> lock(mu);
+    cache[key] = n;
+    *slots = n;
+    return STENCIL_OK;
 }
 
 namespace {
@@ -448,6 +477,30 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
                        : launch_temporalk(*l, in, out, begin, end, steps, as_stream(stream));
     if (rc == STENCIL_OK) clear_error();
     return rc;
+}
+
+int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end, int32_t steps, int64_t* workgroups,
+                            int32_t* zchunk, int32_t* packed) {
+    if (int rc = check_layout(l)) return rc;
+    if (!temporal2_supports(l->prob) || steps < 3 || steps > 5)
+        return set_error(STENCIL_EUNSUPPORTED, "geometry: the K-step kernel of the 3D r=1 7-point star, steps 3..5");
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range out of bounds");
+    const char* strip = std::getenv("STENCIL_TK_STRIP");
+    if (strip && *strip && std::atoi(strip) == 0)  // the interleaved-row kernel has no dry mode
+        return set_error(STENCIL_EUNSUPPORTED, "geometry: not the strip kernel (STENCIL_TK_STRIP=0)");
+    LaunchInfo info;
+    tl_dry_launch = &info;
+    // in/out are never touched in a dry launch
+    const int rc = launch_temporalk(*l, nullptr, reinterpret_cast<void*>(uintptr_t(1)), begin, end, steps, nullptr);
+    tl_dry_launch = nullptr;
+    if (rc != STENCIL_OK) return rc;
+    if (info.steps == 0) return set_error(STENCIL_EUNSUPPORTED, "geometry: no strip launch was described");
+    if (workgroups) *workgroups = info.workgroups;
+    if (zchunk) *zchunk = info.zchunk;
+    if (packed) *packed = info.packed;
+    clear_error();
+    return STENCIL_OK;
 }
 
 int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,

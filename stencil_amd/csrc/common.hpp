@@ -30,6 +30,16 @@ int set_error(int code, const char* fmt, ...);
 // Clear the per-thread error state (success).
 void clear_error();
 
+// Workgroup slots of `kern` (launched with `threads` threads) on the CURRENT
+// device: CUs x resident workgroups per CU (one_per_cu: CUs only).  Cached
+// per (device, kernel) under a lock -- one process may drive several GPUs
+// from several threads (stencil_set_device is per thread).
+int resident_slots(const void* kern, int threads, bool one_per_cu, int* slots);
+template <typename F>
+inline int resident_slots(F* kern, int threads, int* slots) {
+    return resident_slots(reinterpret_cast<const void*>(kern), threads, false, slots);
+}
+
 #define STENCIL_HIP_CHECK(expr)                                                              \
     do {                                                                                     \
         hipError_t e_ = (expr);                                                              \
@@ -58,6 +68,17 @@ inline T avg_weight(const stencil_problem& p) {
     }
     return T(1) / T(2 * p.dims * p.radius);
 }
+
+// Launch geometry of the K-step strip kernel, filled instead of launching
+// while a LaunchInfo is installed for the calling thread
+// (stencil_sweepk_geometry).
+struct LaunchInfo {
+    int64_t workgroups = 0;
+    int zchunk = 0;   // planes per z-chunk; 0 = one balanced share per workgroup
+    int packed = 0;   // the packed longest-first schedule is used
+    int steps = 0;
+};
+extern thread_local LaunchInfo* tl_dry_launch;
 
 // ---- kernel entry points (defined in kernels_*.hip) ----------------------
 int launch_direct(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

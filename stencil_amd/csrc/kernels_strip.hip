@@ -41,6 +41,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <tuple>
 #include <vector>
 
@@ -406,16 +407,23 @@ int64_t simulate_makespan(const std::vector<int>& len, int K, int slots) {
 // one with the shortest simulated makespan; used only when it beats the
 // equal-chunk grid (zc planes per chunk) by 2 %.  The table is built once per
 // shape and kept for the process.
-int packed_schedule(int64_t tiles, int64_t nz, int K, int slots, int zc, const int** sched, int64_t* nb) {
+// The table lives in the memory of the device it was built on: the cache is
+// keyed by device ordinal and guarded (a process may drive several GPUs from
+// several threads: stencil_set_device is per thread).
+int packed_schedule(int dev, int64_t tiles, int64_t nz, int K, int slots, int zc, const int** sched, int64_t* nb) {
     // Only grids of few tiles: with more than 2 tiles per slot the equal
     // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
     // Gcell/s), and the search would cost host time at the first launch.
     if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
-    static std::map<std::tuple<int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
-    const auto key = std::make_tuple(tiles, nz, K, slots);
+    if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
+    static std::mutex mu;
+    static std::map<std::tuple<int, int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_tuple(dev, tiles, nz, K, slots);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
         auto build = [&](int64_t lc, std::vector<int>& tab) {
+            lc = std::max<int64_t>(1, lc);
             struct Item { int len, c, t, z; };
             std::vector<Item> items;
             for (int64_t t = 0; t < tiles; ++t)
@@ -475,20 +483,14 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
     auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS>;
     const int64_t tiles = gx * gy;
+    int dev = 0, slots = 0;
+    STENCIL_HIP_CHECK(hipGetDevice(&dev));
+    if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
     int zc = senv_int("STENCIL_TK_ZCHUNK", 0);
     int64_t nb = 0;
     if (zc > 0) {
         nb = tiles * ((nz + zc - 1) / zc);  // fixed chunks (tests: seams, short chunks)
     } else {
-        static int slots = 0;
-        if (!slots) {
-            int dev = 0, cus = 0, per_cu = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
-                return set_error(STENCIL_EHIP, "occupancy query failed");
-            slots = std::max(1, cus * std::max(1, per_cu));
-        }
         if (!SIG && senv_int("STENCIL_TK_BALANCE", 0)) {
             // one equal share of the (tile, z) units per slot, each share at
             // least 4K planes long (a segment costs 2K planes of pipeline fill).
@@ -499,6 +501,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
             // L2 / Infinity Cache.  Chunk rounds keep all tiles of a chunk in
             // z lock-step.
             nb = std::max<int64_t>(1, std::min<int64_t>(slots, tiles * nz / (4 * K)));
+            zc = 0;  // one equal share per workgroup (the kernel's zchunk == 0 mode); never packed
         } else {
             // whole chunks: the count minimising rounds x (chunk + 2K)
             int64_t best_c = 1, best = INT64_MAX;
@@ -540,14 +543,9 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     // default: the packed longest-first schedule when it beats equal chunks
     // (512^3 fp64 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a
     // multi-GPU job, whose one-round grid above is deliberate
-    if (!SIG && senv_int("STENCIL_TK_PACK", 1) && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
+    if (!SIG && zc > 0 && senv_int("STENCIL_TK_PACK", 1) && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
         !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
-            return set_error(STENCIL_EHIP, "occupancy query failed");
-        const int rc = packed_schedule(gx * gy, nz, K, std::max(1, cus * std::max(1, per_cu)), zc, &sched, &nb);
+        const int rc = packed_schedule(dev, gx * gy, nz, K, slots, zc, &sched, &nb);
         if (rc != STENCIL_OK) return rc;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
@@ -561,6 +559,13 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((lo || hi) && l.zghost < K)
         return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
                          (long long)l.zghost);
+    if (LaunchInfo* info = tl_dry_launch) {  // stencil_sweepk_geometry: describe, do not launch
+        info->workgroups = nb;
+        info->zchunk = zc;
+        info->packed = sched != nullptr;
+        info->steps = K;
+        return STENCIL_OK;
+    }
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
                        avg_weight<T>(l.prob), sig, fsig, sched);
@@ -601,9 +606,12 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 216: return launch_st<double, 2, 2, 16, 3, false>(l, in, out, begin, end, s);
             case 10808: return launch_st<double, 1, 8, 8, 3>(l, in, out, begin, end, s);
             case 10608: return launch_st<double, 1, 6, 8, 3>(l, in, out, begin, end, s);
+#ifdef STENCIL_DIAG
+            // timing experiments only, results wrong on purpose: never in the product build
             case 91: return launch_st<double, 2, 4, 8, 3, true, 1>(l, in, out, begin, end, s);
             case 92: return launch_st<double, 2, 4, 8, 3, true, 2>(l, in, out, begin, end, s);
             case 93: return launch_st<double, 2, 4, 8, 3, true, 3>(l, in, out, begin, end, s);
+#endif
             default: return launch_st<double, 2, 4, 8, 3>(l, in, out, begin, end, s);
             }
         }

@@ -208,12 +208,9 @@ int launch_tb1(const stencil_layout& l, const void* in, void* out, uint32_t iter
     const Geom g = geom_of(l);
     const size_t lds = size_t(2) * size_t(g.nx + 2 * R) * size_t(g.ny + 2 * R) * sizeof(T);
     auto kern = tb2d1<T, ORDER, R>;
-    static bool attr = false;
-    if (!attr) {
-        STENCIL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    // per device and cheap: set it on every launch (a process may drive several GPUs)
+    STENCIL_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     hipLaunchKernelGGL(kern, dim3(1), dim3(k1Threads), lds, s, static_cast<const T*>(in), static_cast<T*>(out), g,
                        int(iterations), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
@@ -329,16 +326,8 @@ namespace {
 // two strip workgroups per CU, but measured rounds behave as one per CU (C1
 // fp64: 240 tiles 658 Gcell/s, 260 tiles 571), so the CU count it is.
 int strip_slots() {
-    static int slots = -1;
-    if (slots < 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            slots = 0;
-        else
-            slots = cus;
-    }
-    return slots;
+    int slots = 0;  // per device (resident_slots caches it); 0 when the query fails
+    return resident_slots(reinterpret_cast<const void*>(&strip_slots), 0, true, &slots) == STENCIL_OK ? slots : 0;
 }
 }  // namespace
 

@@ -111,9 +111,14 @@ int launch_tbp(const stencil_layout& l, void* a, void* b, uint32_t iterations, i
     if (TX < 4 || TY < 4 || TX < H || TY < H)
         return set_error(STENCIL_EUNSUPPORTED, "tb2dp: %d steps of radius %d leave no tile", K, R);
     const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
+#ifdef STENCIL_DIAG
+    // timing experiments only (results wrong on purpose): never in the product build
     static const int diag = [] { const char* e = std::getenv("STENCIL_TB2DP_DIAG"); return e ? std::atoi(e) : 0; }();
     auto kern = diag == 1 ? tb2dp<T, ORDER, R, V, RY, NW, 1> : diag == 2 ? tb2dp<T, ORDER, R, V, RY, NW, 2>
                                                                          : tb2dp<T, ORDER, R, V, RY, NW, 0>;
+#else
+    auto kern = tb2dp<T, ORDER, R, V, RY, NW, 0>;
+#endif
     int dev = 0, cus = 0, per_cu = 0, coop = 0;
     STENCIL_HIP_CHECK(hipGetDevice(&dev));
     STENCIL_HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));

@@ -301,15 +301,8 @@ int launch_tk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         // planes, and a last round that is mostly empty costs as much as a
         // full one (measured, 512^3 fp64: zc 103 / 52 -> 2 / 3.9 rounds
         // 885 Gcell/s, zc 64 / 128 -> 3.1 / 1.6 rounds 760-790).
-        static int slots = 0;
-        if (!slots) {
-            int dev = 0, cus = 0, per_cu = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess)
-                return set_error(STENCIL_EHIP, "occupancy query failed");
-            slots = std::max(1, cus * std::max(1, per_cu));
-        }
+        int slots = 0;
+        if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
         const int64_t tiles = gx * gy;
         int64_t best_c = 1, best = INT64_MAX;
         for (int64_t c = 1; c <= nz; ++c) {

@@ -78,8 +78,8 @@ class JacobiEngine:
         # 3 (or 4) for the 7-point star (TEMPORALK), 2 for the 27-point box
         self.fuse_steps = 1
         if self.fused:
-            launches, _ = self.plan(12)
-            self.fuse_steps = 12 // launches if launches and 12 % launches == 0 else 2
+            # sweeps per fused launch: the most sweeps stencil_iterate runs as one launch
+            self.fuse_steps = next((k for k in (5, 4, 3, 2) if self.plan(k)[0] == 1), 2)
         self.slow_extent = int(self.lib.stencil_slow_extent(ctypes.byref(self.layout)))
         # one slow-axis unit = a whole plane (3D) or a whole padded row (2D)
         self.unit = int(self.layout.plane if spec.dims == 3 else self.layout.row)
@@ -115,6 +115,15 @@ class JacobiEngine:
         _lib.check(self.lib.stencil_sweepk(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
                                            _stream_handle(stream)), "stencil_sweepk")
+
+    def sweepk_geometry(self, steps: int, begin: int = 0, end: int | None = None) -> dict:
+        """How sweepk(steps) over [begin, end) would launch the K-step strip
+        kernel: workgroups, planes per z-chunk, packed schedule or not."""
+        wg, zc, packed = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        end = self.slow_extent if end is None else end
+        _lib.check(self.lib.stencil_sweepk_geometry(ctypes.byref(self.layout), begin, end, steps, ctypes.byref(wg),
+                                                    ctypes.byref(zc), ctypes.byref(packed)), "stencil_sweepk_geometry")
+        return {"workgroups": int(wg.value), "zchunk": int(zc.value), "packed": bool(packed.value)}
 
     @property
     def supports_signal(self) -> bool:

@@ -208,6 +208,15 @@ class SlabJacobi:
         [b, e); `edge` = boundary planes updated first on each side."""
         src, dst = self.cur, self.nxt
         n = self.slab.count
+        serial = self.slab.world == 1 or not self.overlap or n <= 2 * edge or not self.on_gpu
+        if serial:
+            # These branches launch on the caller's stream: join the round
+            # streams first.  A remainder pair/single after face-signalled
+            # rounds otherwise reads src while the last signalled launch on
+            # stream_int still writes it, and its halos while the exchange on
+            # stream_bnd still receives them (the nz = 2K failures of
+            # test_signalled_rounds_every_k, round 1).
+            self.finish()
         if self.slab.world == 1:
             update(src, dst, 0, n, None)
         elif not self.overlap or n <= 2 * edge:

@@ -54,6 +54,46 @@ def test_golden_fixtures(gpu, name, kernel):
     assert same_bits(np.ascontiguousarray(ob.interior(p, g)), fx[name])
 
 
+def _ref_fixture_cases():
+    return sorted(np.load(os.path.join(GOLD, "ref_fixtures.npz")).files)
+
+
+@pytest.mark.parametrize("name", _ref_fixture_cases())
+@pytest.mark.parametrize("kernel", ["direct", "auto"])
+def test_reference_build_fixtures(gpu, name, kernel):
+    """Outputs of the reference's OWN compiled naive loop (oracle/ref/build.sh,
+    tests/golden/make_ref_golden.py) -- the HIP kernels bit for bit."""
+    a = np.load(os.path.join(GOLD, "ref_fixtures.npz"))[name]
+    n, it, r, dt = name.split("_")
+    n, it, r = int(n[1:]), int(it[1:]), int(r[1:])
+    dtype = "fp64" if dt == "f64" else "fp32"
+    e, g = gpu_run(gpu, 2, dtype, "star", r, "naive", kernel, n, n, 1, it)
+    p = ob.problem(2, dtype, "star", r, "naive", n, n)
+    assert same_bits(np.ascontiguousarray(ob.interior(p, g)), np.ascontiguousarray(a))
+
+
+@pytest.mark.parametrize("name", [c for c in _ref_fixture_cases() if c.endswith("f32") and "_r1_" in c])
+def test_reference_build_fixtures_static_unroll_abi(gpu, name):
+    """The drop-in entry point stencil_iterate_dma_static_unroll (the reference
+    variant whose sum order is the naive loop's), host buffers,
+    parity-selected output -- equal to the reference build's bytes."""
+    from stencil_amd import _lib
+    lib = _lib.load()
+    want = np.load(os.path.join(GOLD, "ref_fixtures.npz"))[name]
+    n, it = int(name.split("_")[0][1:]), int(name.split("_")[1][1:])
+    p = ob.problem(2, "fp32", "star", 1, "naive", n, n)
+    a = ob.init(p)
+    b = a.copy()
+
+    def view(arr):
+        return _lib.MatrixView(n + 2, n + 2, 1, 1, n + 2, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    args = _lib.Arguments(max(1, (n + 7) // 8), it, view(a), view(b))
+    lib.stencil_iterate_dma_static_unroll(ctypes.byref(args))
+    assert lib.stencil_last_error() == 0, lib.stencil_last_error_message()
+    got = np.ascontiguousarray(ob.interior(p, b if it % 2 else a))
+    assert same_bits(got, np.ascontiguousarray(want))
+
+
 # ------------------------------------------------ reference configs (2D)
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("order", ["naive", "dma"])
@@ -254,6 +294,28 @@ def test_tkstrip_chunking(gpu, monkeypatch, steps, strip, zchunk, dtype, shape3)
         assert same_bits(got, want), it
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_tkstrip_packed_schedule_small_shapes(gpu, dtype):
+    """The default K-step launch (packed longest-first z-chunks where the
+    host's makespan model picks them) at shapes of few tiles, bitwise against
+    the oracle; the geometry query shows which launches were packed, and at
+    least one of these shapes must be."""
+    shapes = [(131, 61, 29), (200, 200, 200), (300, 200, 150), (512, 512, 96), (600, 100, 64), (64, 7, 90)]
+    packed = []
+    for nx, ny, nz in shapes:
+        e = engine(gpu, 3, dtype, "star", 1, "naive", "auto", nx, ny, nz)
+        k = e.fuse_steps
+        geo = e.sweepk_geometry(k)
+        packed.append(geo["packed"])
+        it = 2 * k + 1
+        p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+        want = ob.run(p, it, "random", 31)
+        e.reset("random", 31)
+        fin, _ = e.iterate(it)
+        assert same_bits(e.to_numpy(fin), want), ((nx, ny, nz), geo)
+    assert any(packed), list(zip(shapes, packed))
+
+
 @pytest.mark.parametrize("cfg", ["default", "308", "216", "1116", "208", "116", "1416", "1216"])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
@@ -415,6 +477,38 @@ def test_full_size_baseline_configs(gpu, cfg):
     assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
     del e
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case", ["C2_512cube_fp64", "C3_4096sq_x32_fp32", "C4_2048sq_x512_fp64"])
+def test_benched_kernel_at_benched_shape(gpu, case):
+    """The kernels that produce the bench numbers, at the shapes they are
+    benched on, through AUTO, bitwise against the multithreaded oracle --
+    with the plan asserted, so the tested launch IS the benched one:
+      C2: 512^3 fp64, 9 sweeps = two K = 4 strip launches with the packed
+          longest-first schedule + a single sweep (bench.py's default line);
+      C3: 4096^2 x 32 fp32, 10 sweeps = two K = 5 launches (AUTO's K for fp32
+          planes >= 1024^2);
+      C4: 2048^2 x 512 fp64 (one GPU's slab of config 4), 8 sweeps = two
+          K = 4 launches of equal z-chunks (too many tiles to pack)."""
+    import torch
+    from stencil_amd import _lib
+    shapes = {"C2_512cube_fp64": ("fp64", (512, 512, 512), 9, 4, (3, _lib.KERNEL_TEMPORALK), True),
+              "C3_4096sq_x32_fp32": ("fp32", (4096, 4096, 32), 10, 5, (2, _lib.KERNEL_TEMPORALK), False),
+              "C4_2048sq_x512_fp64": ("fp64", (2048, 2048, 512), 8, 4, (2, _lib.KERNEL_TEMPORALK), False)}
+    dtype, (nx, ny, nz), it, k, plan, packed = shapes[case]
+    e = engine(gpu, 3, dtype, "star", 1, "naive", "auto", nx, ny, nz)
+    assert e.fuse_steps == k
+    assert e.plan(it) == plan
+    geo = e.sweepk_geometry(k)
+    assert geo["packed"] == packed, geo
+    e.reset("random", 4242)
+    fin, _ = e.iterate(it)
+    got = e.interior(fin).cpu().numpy()
+    del e, fin
+    torch.cuda.empty_cache()
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    want = ob.interior(p, ob.run(p, it, "random", 4242, threads=16))
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
 
 
 # ------------------------------------------- reference-compatible entry points

@@ -288,6 +288,24 @@ def test_signalled_rounds_every_k(gpu, monkeypatch, dtype, steps, extra, it):
     assert torch.equal(got.view(ib), want.view(ib)), (nz, it)
 
 
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_signalled_rounds_then_remainder_large_plane(gpu, dtype):
+    """The round-1 stream race, made deterministic: a minimum slab (nz = 2K)
+    with a 2048^2 plane, so the last face-signalled launch runs for
+    milliseconds, then a remainder pair.  The pair runs on the caller's
+    stream (n <= 2*edge), which must first join the round streams -- it
+    reads the grid the last signalled launch writes and the halos the
+    exchange receives.  Bitwise the boundary + interior rounds."""
+    from stencil_amd.slab import LoopbackExchanger
+    nx = ny = 2048
+    fuse = JacobiEngine(StencilSpec(dims=3, dtype=dtype), nx, ny, 8, device=gpu, allocate=False).fuse_steps
+    nz, it = 2 * fuse, 2 * fuse + 2  # two signalled rounds + a remainder pair
+    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype)
+    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, False, dtype=dtype)
+    ib = torch.int64 if dtype == "fp64" else torch.int32
+    assert torch.equal(got.view(ib), want.view(ib))
+
+
 def test_signalled_rounds_over_rccl(gpu):
     """The same through RCCL send/recv to self (world size 1)."""
     import os

@@ -1,8 +1,18 @@
-"""Pin the CPU oracle (oracle/) against the reference's known answers
-(tests/golden/survey_known_answers.json) and freeze it with
-the committed fixtures (tests/golden/oracle_fixtures.npz)."""
+"""Pin the CPU oracle (oracle/) against the reference's own code and freeze it.
+
+1. tests/golden/ref_fixtures.npz + ref_known_answers.json: outputs of the
+   reference's naive loop (src/stencil/stencil.cpp:77-131, 190-207) compiled
+   from /root/reference by oracle/ref/build.sh (tests/golden/make_ref_golden.py)
+   -- bit for bit, including C1 (1024^2, 100 sweeps) and 400^2 x 1000 by sha256.
+2. The survey's recorded known answers (SURVEY.md §8c,
+   tests/golden/survey_known_answers.json): sums, spot values, the DMA order's
+   deviation statistics.
+3. The frozen oracle fixtures (tests/golden/oracle_fixtures.npz): 3D, box,
+   random interiors -- shapes the reference has no code for (parity unpinned)."""
+import hashlib
 import json
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -11,6 +21,45 @@ from oracle import binding as ob
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 KA = json.load(open(os.path.join(GOLD, "survey_known_answers.json")))
+REF = json.load(open(os.path.join(GOLD, "ref_known_answers.json")))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _oracle_interior(case):
+    dt = "fp64" if case["dtype"] == "f64" else "fp32"
+    p = ob.problem(2, dt, radius=case["radius"], nx=case["n"], ny=case["n"])
+    return np.ascontiguousarray(ob.interior(p, ob.run(p, case["iterations"], threads=4)))
+
+
+@pytest.mark.parametrize("case", REF["cases"], ids=lambda c: c["name"])
+def test_oracle_bitwise_equals_reference_build(case):
+    """The oracle's interior bytes hash to exactly what the reference's own
+    compiled loop produced (sha256), for every recorded case."""
+    got = _oracle_interior(case)
+    assert hashlib.sha256(got.tobytes()).hexdigest() == case["sha256"]
+
+
+def test_oracle_equals_reference_fixtures():
+    fx = np.load(os.path.join(GOLD, "ref_fixtures.npz"))
+    by_name = {c["name"]: c for c in REF["cases"]}
+    assert len(fx.files) >= 16
+    for name in fx.files:
+        got = _oracle_interior(by_name[name])
+        assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(fx[name]).view(np.uint8)), name
+
+
+@pytest.mark.skipif(not os.path.isfile("/root/reference/src/stencil/stencil.cpp"),
+                    reason="the reference tree exists in the build container only")
+def test_reference_build_reproduces_fixtures():
+    """oracle/ref/build.sh rebuilds the reference's loop and the ABI layout
+    check (static_asserts against the real Arguments / BoundaryMatrixView);
+    the rebuilt binary reproduces two committed cases bit for bit."""
+    subprocess.run(["bash", os.path.join(ROOT, "oracle", "ref", "build.sh")], check=True, capture_output=True)
+    fx = np.load(os.path.join(GOLD, "ref_fixtures.npz"))
+    for name, (n, it, r, dt) in {"n96_i50_r3_f32": (96, 50, 3, "f32"), "n64_i100_r1_f64": (64, 100, 1, "f64")}.items():
+        out = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_naive"), str(n), str(it), str(r), dt],
+                             check=True, capture_output=True).stdout
+        assert out == np.ascontiguousarray(fx[name]).tobytes(), name
 
 
 @pytest.mark.parametrize("case", KA["fp32_naive_sums"], ids=lambda c: f"n{c['n']}_i{c['iterations']}_r{c['radius']}")

@@ -61,10 +61,14 @@ def main():
     json.dump(summary, open(os.path.join(ROOT, "profiles", f"{tag}_summary.json"), "w"), indent=1)
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     table = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_sha  # the sources the profiled library was built from
     for k, ent in summary["kernels"].items():
-        if "hbm_bytes_per_launch" in ent and k in ("temporalk", "temporal2", "zmarch", "direct"):
+        if "hbm_bytes_per_launch" in ent and k in ("temporalk", "temporal2", "zmarch", "direct", "boxk"):
             table.setdefault(workload, {})[k] = {"hbm_bytes_per_launch": round(ent["hbm_bytes_per_launch"]),
-                                                 "source": f"profiles/{tag}_summary.json"}
+                                                 "source": f"profiles/{tag}_summary.json",
+                                                 "kernel": ent["name"],
+                                                 "kernel_source_sha": kernel_source_sha(k)}
     json.dump(table, open(tpath, "w"), indent=1)
     for k, ent in summary["kernels"].items():
         print(k, {x: round(y, 1) if isinstance(y, float) else y for x, y in ent.items() if x != "name"})
