@@ -254,6 +254,47 @@ int stencil_plane_sums(const stencil_layout* l, const void* dev, double* plane_s
 int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, void* stream,
                            float* elapsed_ms);
 
+/* ------------------------------------------------ 3. multi-GPU z-slab jobs
+ *
+ * The reference runs its whole decomposed job behind one call: 64 CPEs own
+ * 8x8 blocks and exchange halo strips every iteration (athread_spawn/join,
+ * src/stencil/stencil.cpp:34-53; stencil_dma.cpp:236-247, stencil_rma.cpp:
+ * 198-255).  A slab job does the same across GPUs from ONE host thread: the
+ * global 3D grid is cut into contiguous z-slabs (remainder planes to the
+ * lowest slabs), slab i lives on devices[i] with K ghost planes per shared
+ * face (K = the sweeps stencil_iterate fuses into one launch for `global`),
+ * and every round of K fused sweeps exchanges K whole planes with each
+ * neighbour: the boundary planes first on a high-priority stream with the
+ * exchange behind them, the interior on a second stream.  Results are bitwise
+ * those of one grid.  Exchange: RCCL ncclSend/ncclRecv (ncclCommInitAll over
+ * the devices, one slab per GPU; librccl is loaded on first use) or device
+ * copies (hipMemcpyPeerAsync; slabs may share a GPU).  PERIODIC joins the
+ * two z ends into a ring (a rehearsal mode: one slab exchanges with itself). */
+enum { STENCIL_EXCHANGE_RCCL = 0, STENCIL_EXCHANGE_COPY = 1 };
+enum { STENCIL_SLAB_PERIODIC = 1 };
+typedef struct stencil_slab_job stencil_slab_job;
+
+/* global: a 3D problem with halo = 0 and flags = 0; devices: ngpus ordinals
+ * (NULL = 0 .. ngpus-1).  Every slab must own at least K planes. */
+int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange,
+                        int32_t flags, stencil_slab_job** job);
+int stencil_slab_destroy(stencil_slab_job* job);
+int stencil_slab_info(const stencil_slab_job* job, int32_t slab, int64_t* first_plane, int64_t* planes,
+                      int32_t* device, int32_t* sweeps_per_round);
+/* Initial condition of the global grid (global linear indices for the random
+ * interior, as stencil_fill_initial on one grid), halos exchanged. */
+int stencil_slab_fill_initial(stencil_slab_job* job, int32_t init_kind, uint64_t seed);
+/* The global grid from / to a dense host array with ghosts (x fastest,
+ * host_row elements per row, host_rows rows per plane, nz + 2r planes). */
+int stencil_slab_upload(stencil_slab_job* job, const void* host, int64_t host_row, int64_t host_rows);
+int stencil_slab_download(stencil_slab_job* job, void* host, int64_t host_row, int64_t host_rows);
+/* `iterations` sweeps of the whole job (rounds of K, the remainder as one
+ * shorter round); synchronous.  elapsed_ms: host wall time of the rounds,
+ * all devices synchronised at both ends. */
+int stencil_slab_run(stencil_slab_job* job, uint32_t iterations, float* elapsed_ms);
+/* Per-plane interior sums of the current global grid (nz doubles, host). */
+int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 F32, F64 = 0, 1
 STAR, BOX = 0, 1
-NAIVE, DMA = 0, 1
+NAIVE, DMA, LEX = 0, 1, 2
 
 
 class Problem(ctypes.Structure):
@@ -51,7 +51,7 @@ def load():
 
 def problem(dims=2, dtype="fp32", shape="star", radius=1, order="naive", nx=1, ny=1, nz=1) -> Problem:
     return Problem(dims, F64 if dtype == "fp64" else F32, BOX if shape == "box" else STAR, radius,
-                   DMA if order == "dma" else NAIVE, 0, nx, ny, nz if dims == 3 else 1)
+                   {"dma": DMA, "lex": LEX}.get(order, NAIVE), 0, nx, ny, nz if dims == 3 else 1)
 
 
 def dense_shape(p: Problem):

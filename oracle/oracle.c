@@ -36,8 +36,9 @@ int oracle_check(const oracle_problem* p) {
     if (p->dtype != ORACLE_F32 && p->dtype != ORACLE_F64) return -3;
     if (p->shape != ORACLE_STAR && p->shape != ORACLE_BOX) return -4;
     if (p->radius < 1) return -5;
-    if (p->order != ORACLE_ORDER_NAIVE && p->order != ORACLE_ORDER_DMA) return -6;
+    if (p->order != ORACLE_ORDER_NAIVE && p->order != ORACLE_ORDER_DMA && p->order != ORACLE_ORDER_LEX) return -6;
     if (p->order == ORACLE_ORDER_DMA && (p->dims != 2 || p->shape != ORACLE_STAR)) return -6;
+    if (p->order == ORACLE_ORDER_LEX && p->shape != ORACLE_BOX) return -6;
     if (p->nx < 0 || p->ny < 0 || (p->dims == 3 && p->nz < 0)) return -7;
     return 0;
 }

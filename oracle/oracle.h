@@ -43,7 +43,10 @@ extern "C" {
 
 enum { ORACLE_F32 = 0, ORACLE_F64 = 1 };
 enum { ORACLE_STAR = 0, ORACLE_BOX = 1 };
-enum { ORACLE_ORDER_NAIVE = 0, ORACLE_ORDER_DMA = 1 };
+/* ORACLE_ORDER_LEX: the box's round-1 definition (26 terms added in
+ * lexicographic (dz, dy, dx) order), kept only to show the separable order
+ * (the box's definition, oracle_impl.inc) agrees with it to ~1e-15 relative. */
+enum { ORACLE_ORDER_NAIVE = 0, ORACLE_ORDER_DMA = 1, ORACLE_ORDER_LEX = 2 };
 enum { ORACLE_INIT_REFERENCE = 0, ORACLE_INIT_RANDOM = 1 };
 
 typedef struct {
@@ -51,7 +54,7 @@ typedef struct {
     int32_t dtype;  /* ORACLE_F32 / ORACLE_F64 */
     int32_t shape;  /* ORACLE_STAR / ORACLE_BOX */
     int32_t radius; /* >= 1 */
-    int32_t order;  /* ORACLE_ORDER_NAIVE / ORACLE_ORDER_DMA (2D star only) */
+    int32_t order;  /* ORACLE_ORDER_NAIVE / ORACLE_ORDER_DMA (2D star only) / ORACLE_ORDER_LEX (box only) */
     int32_t reserved;
     int64_t nx, ny, nz; /* interior extents; nz ignored for 2D */
 } oracle_problem;

@@ -20,6 +20,8 @@ ORDER_NAIVE, ORDER_DMA = 0, 1
 KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2, KERNEL_TEMPORALK, KERNEL_PERSISTENT = 0, 1, 2, 3, 4, 5
 INIT_REFERENCE, INIT_RANDOM = 0, 1
 HALO_LO, HALO_HI = 1, 2
+EXCHANGE_RCCL, EXCHANGE_COPY = 0, 1
+SLAB_PERIODIC = 1
 
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2,
                 "temporalk": KERNEL_TEMPORALK, "persistent": KERNEL_PERSISTENT}
@@ -35,6 +37,8 @@ EXPORTED_SYMBOLS = (
     "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth", "stencil_sweepk_geometry", "stencil_sweepk_signal",
     "stencil_wait_counters", "stencil_face_signal_create", "stencil_face_signal_destroy",
     "stencil_face_signal_reset", "stencil_face_signal_read", "stencil_wait_face_signal",
+    "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
+    "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
 )
 
 
@@ -115,6 +119,16 @@ def load() -> ctypes.CDLL:
         "stencil_face_signal_reset": (c_int, [c_void_p, c_void_p]),
         "stencil_face_signal_read": (c_int, [c_void_p, POINTER(c_uint64)]),
         "stencil_wait_face_signal": (c_int, [c_void_p, c_uint64, c_void_p]),
+        "stencil_slab_create": (c_int, [POINTER(Problem), c_int32, POINTER(c_int32), c_int32, c_int32,
+                                        POINTER(c_void_p)]),
+        "stencil_slab_destroy": (c_int, [c_void_p]),
+        "stencil_slab_info": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32),
+                                      POINTER(c_int32)]),
+        "stencil_slab_fill_initial": (c_int, [c_void_p, c_int32, c_uint64]),
+        "stencil_slab_upload": (c_int, [c_void_p, c_void_p, c_int64, c_int64]),
+        "stencil_slab_download": (c_int, [c_void_p, c_void_p, c_int64, c_int64]),
+        "stencil_slab_run": (c_int, [c_void_p, c_uint32, POINTER(c_float)]),
+        "stencil_slab_plane_sums": (c_int, [c_void_p, POINTER(c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

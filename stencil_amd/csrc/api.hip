@@ -166,12 +166,10 @@ int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b,
     return launch_direct(l, in, out, b, e, s);
 }
 
-// Two fused sweeps.  27-point box: the two-phase K-step kernel
-// (kernels_boxk.hip); STENCIL_BOXK=0 selects the earlier box27_zmarch<2>.
+// Two fused sweeps.  27-point box: the separable-sum z-march
+// (kernels_boxk.hip), K = 2.
 int launch_fused(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
     if (temporal2_supports(l.prob)) return launch_temporal2(l, in, out, b, e, s);
-    const char* k = std::getenv("STENCIL_BOXK");
-    if (k && *k == '0') return launch_box27(l, in, out, b, e, 2, s);
     return launch_boxk(l, in, out, b, e, 2, s);
 }
 

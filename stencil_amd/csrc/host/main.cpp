@@ -98,7 +98,8 @@ int main(int argc, char** argv) {
                       << " dims=" << options->dims << " nx=" << options->extent_x() << " ny=" << options->extent_y()
                       << " nz=" << options->extent_z() << " dtype=" << (options->fp64 ? "fp64" : "fp32")
                       << " shape=" << (options->box ? "box" : "star") << " kernel=" << options->kernel
-                      << " init=" << (options->random_init ? "random" : "reference") << " methods=";
+                      << " init=" << (options->random_init ? "random" : "reference") << " gpus=" << options->gpus
+                      << " exchange=" << (options->exchange_copy ? "copy" : "rccl") << " methods=";
             for (size_t i = 0; i < options->method_names.size(); ++i)
                 std::cout << (i ? "," : "") << options->method_names[i];
             std::cout << "\n";

@@ -127,6 +127,12 @@ auto ProgramOptions::parse(int argc, char** argv) -> std::optional<ProgramOption
          [&](const std::string& v) { r.bmp = v; return !v.empty(); }},
         {0, "seed", Kind::Int64, false, "[ext] Seed of --init random.",
          [&](const std::string& v) { int64_t s; if (!parse_i64(v, s)) return false; r.seed = uint64_t(s); return true; }},
+        {0, "gpus", Kind::Int, false, "[ext] 3D: split the grid into z-slabs over N GPUs (one host thread, RCCL halos).",
+         [&](const std::string& v) { int64_t g; if (!parse_i64(v, g) || g < 1 || g > 64) return false; r.gpus = int(g); return true; }},
+        {0, "exchange", Kind::Str, false, "[ext] Halo transport of --gpus jobs: rccl (default) or copy (device copies).",
+         [&](const std::string& v) { if (v != "rccl" && v != "copy") return false; r.exchange_copy = v == "copy"; return true; }},
+        {0, "share-device", Kind::Flag, false, "[ext] Put every slab of a --gpus job on --device (rehearsal; --exchange copy).",
+         [&](const std::string&) { r.share_device = true; return true; }},
     };
 
     auto find_long = [&](const std::string& n) -> Opt* {

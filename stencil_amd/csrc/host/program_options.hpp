@@ -39,6 +39,9 @@ struct ProgramOptions {
     uint64_t seed = 0x5EED;        // --seed N
     bool print_config = false;     // --print-config: print the parsed options and exit 0
     std::string bmp;               // --bmp FILE: dump the final grid of each method (f4)
+    int gpus = 1;                  // --gpus N: 3D z-slab job over N GPUs (devices device .. device+N-1)
+    bool exchange_copy = false;    // --exchange rccl|copy: halo transport of --gpus jobs
+    bool share_device = false;     // --share-device: every slab on --device (needs --exchange copy)
 
     int64_t extent_x() const { return nx >= 0 ? nx : matrix_size; }
     int64_t extent_y() const { return ny >= 0 ? ny : matrix_size; }

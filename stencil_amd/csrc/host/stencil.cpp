@@ -81,10 +81,54 @@ void Stencil::initialize_matrix() {
     else init_typed(matrix32, result32);
 }
 
+// The job as z-slabs over several GPUs (HIPMultiGPU, or any HIP method with
+// --gpus N > 1): one host thread, stencil_slab_* (csrc/slab.hip).  Timed like
+// the single-grid run: the rounds on grids already resident on the GPUs.
+template <class T>
+auto Stencil::run_slabs(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std::chrono::steady_clock::duration {
+    if (options.dims != 3) throw std::runtime_error("--gpus / HIPMultiGPU split 3D grids along z (use --dims 3)");
+    if (options.share_device && !options.exchange_copy)
+        throw std::runtime_error("--share-device needs --exchange copy (RCCL takes one slab per GPU)");
+    stencil_problem p{};
+    p.dims = 3;
+    p.dtype = options.fp64 ? STENCIL_F64 : STENCIL_F32;
+    p.shape = options.box ? STENCIL_BOX : STENCIL_STAR;
+    p.radius = int(options.radius);
+    p.order = STENCIL_ORDER_NAIVE;
+    p.kernel = kernel_of(options.kernel);
+    p.nx = matrix.width();
+    p.ny = matrix.height();
+    p.nz = matrix.depth();
+    std::vector<int32_t> devices(size_t(options.gpus));
+    for (int i = 0; i < options.gpus; ++i) devices[size_t(i)] = options.share_device ? options.device : options.device + i;
+    struct Job {
+        stencil_slab_job* j = nullptr;
+        ~Job() { if (j) stencil_slab_destroy(j); }
+    } job;
+    check(stencil_slab_create(&p, options.gpus, devices.data(),
+                              options.exchange_copy ? STENCIL_EXCHANGE_COPY : STENCIL_EXCHANGE_RCCL, 0, &job.j),
+          "stencil_slab_create");
+    check(stencil_slab_upload(job.j, matrix.data(), matrix.row_stride(), matrix.rows_with_boundary()), "slab upload");
+    if (options.iterations > 0) {  // untimed warm-up (code-object load, RCCL connection setup), then a fresh upload
+        check(stencil_slab_run(job.j, 1, nullptr), "slab warm-up");
+        check(stencil_slab_upload(job.j, matrix.data(), matrix.row_stride(), matrix.rows_with_boundary()), "slab upload");
+    }
+    float ms = 0.f;
+    auto const start = std::chrono::steady_clock::now();
+    check(stencil_slab_run(job.j, options.iterations, &ms), "stencil_slab_run");
+    auto const end = std::chrono::steady_clock::now();
+    device_ms = ms;
+    BoundaryGrid<T>& dst = (options.iterations & 1u) ? result : matrix;  // parity rule, stencil.cpp:88-92,134
+    check(stencil_slab_download(job.j, dst.data(), dst.row_stride(), dst.rows_with_boundary()), "slab download");
+    return end - start;
+}
+
 template <class T>
 auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGrid<T>& result)
     -> std::chrono::steady_clock::duration {
     initialize_matrix();
+    const bool ref_variant = method == DMA || method == DMA_STATIC_UNROLL || method == DMA_SLAVE_PACK || method == RMA;
+    if (method == HIP_MULTI_GPU || (options.gpus > 1 && !ref_variant)) return run_slabs(matrix, result);
 
     stencil_problem p{};
     p.dims = options.dims;
@@ -197,6 +241,7 @@ auto Stencil::run(std::string_view method_name) -> std::optional<std::chrono::st
         {"HIPTemporal2", HIP_TEMPORAL2},
         {"HIPTemporalK", HIP_TEMPORALK},
         {"HIPPersistent", HIP_PERSISTENT},
+        {"HIPMultiGPU", HIP_MULTI_GPU},
     };
     auto const iter = method_map.find(method_name);
     if (iter == method_map.end()) return std::nullopt;
@@ -230,11 +275,30 @@ bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& 
                     const int64_t c = ((z + zr) * in.rows_with_boundary() + (y + r)) * sx + (x + r);
                     T sum = T(0);
                     if (options.box) {
+                        // separable partial sums (no reference code)
                         const int rz = options.dims == 3 ? r : 0;
-                        for (int dz = -rz; dz <= rz; ++dz)
-                            for (int dy = -r; dy <= r; ++dy)
-                                for (int dx = -r; dx <= r; ++dx)
-                                    if (dz || dy || dx) sum += src[c + dz * sxy + dy * sx + dx];
+                        auto rowsum = [&](int64_t q) {
+                            T a = src[q - r];
+                            for (int dx = -r + 1; dx <= r; ++dx) a += src[q + dx];
+                            return a;
+                        };
+                        for (int dz = -rz; dz <= rz; ++dz) {
+                            const int64_t pl = c + dz * sxy;
+                            T term;
+                            if (dz != 0) {
+                                term = rowsum(pl - r * sx);
+                                for (int dy = -r + 1; dy <= r; ++dy) term += rowsum(pl + dy * sx);
+                            } else {
+                                T w = rowsum(pl - r * sx);
+                                for (int dy = -r + 1; dy <= r; ++dy)
+                                    if (dy != 0) w += rowsum(pl + dy * sx);
+                                T e = src[pl - r];
+                                for (int dx = -r + 1; dx <= r; ++dx)
+                                    if (dx != 0) e += src[pl + dx];
+                                term = w + e;
+                            }
+                            sum = dz == -rz ? term : sum + term;
+                        }
                     } else {
                         for (int k = r; k >= 1; --k) sum += src[c - k];       // left
                         for (int k = 1; k <= r; ++k) sum += src[c + k];       // right

@@ -31,6 +31,7 @@ public:
         HIP_TEMPORAL2,      ///< naive order, two fused time steps per launch
         HIP_TEMPORALK,      ///< naive order, 3 or 4 fused time steps per launch (7-point star)
         HIP_PERSISTENT,     ///< naive order, the whole 2D job in one launch (neighbour flags)
+        HIP_MULTI_GPU,      ///< naive order, 3D z-slabs over --gpus GPUs, halos over RCCL (stencil_slab_*)
     };
 
     Stencil() = default;
@@ -62,6 +63,8 @@ private:
     template <class T>
     auto run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGrid<T>& result)
         -> std::chrono::steady_clock::duration;
+    template <class T>
+    auto run_slabs(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std::chrono::steady_clock::duration;
     template <class T>
     bool check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const;
     template <class T>

@@ -1,37 +1,39 @@
-// kernels_boxk.hip -- K fused sweeps per launch of the 3D 27-point box
-// stencil (r = 1, naive order), in the two-phase z-march of
-// kernels_temporalk.hip.
+// kernels_boxk.hip -- the 3D 27-point box stencil (r = 1, naive order):
+// K = 1, 2 or 3 sweeps per launch, z-marching with SEPARABLE partial sums.
 //
-// Sum order.  The reference adds the 26 neighbours lexicographically in
-// (dz, dy, dx) with the centre skipped (oracle/oracle_impl.inc): the 9 terms
-// of plane z-1, then the 8 of plane z, then the 9 of plane z+1.  So while
-// plane q of t_{s-1} sits in LDS, stage s can, for every cell of its column,
-//     finish   t_s(q-1)   (+ its 9 dz=+1 terms)   -> * avg
-//     continue t_s(q)     (+ its 8 dz=0 terms)
-//     start    t_s(q+1)   (its 9 dz=-1 terms)
-// which is every cell's 26 additions in exactly that order, with two running
-// sums per cell (t_s(q), t_s(q+1)) carried in registers between planes.
+// Sum order (no reference code for the box; defined in DESIGN.md §3 and
+// restated by oracle/oracle_impl.inc):
+//     R(y')  = (in[x-1] + in[x]) + in[x+1]          row sum of row y'
+//     E      = in[x-1] + in[x+1]                    centre row without the centre
+//     P9(z') = (R(y-1) + R(y)) + R(y+1)              plane sum of plane z'
+//     C(z)   = (R(y-1) + R(y+1)) + E                 centre plane without the centre
+//     cell   = ((P9(z-1) + C(z)) + P9(z+1)) * avg
+// Row sums are shared by the three cells above / at / below a row, plane sums
+// by the cells below / above a plane: ~11 VALU operations per cell and stage
+// instead of the 26 dependent additions of a lexicographic order.
 //
-// Pipeline.  Stage s finishes plane q-1 at the iteration where its newest
-// input plane is q = p - 2s + 1, and stage s+1 reads that plane one iteration
-// later, so stage s lags stage s-1 by two planes and a chunk [za, zb) runs
-// zb - za + 3K iterations over input planes za-K .. zb+K-1.  Per iteration:
-//   barrier A
-//   read phase   for s = 1..K: the 3x3 neighbourhood of the lane's cells in
-//                LDS plane s-1 (3 vector reads, x neighbours by DPP lane
-//                shifts); finish / continue / start as above.  Intermediate
-//                planes keep ghost cells at their input value (the lane's own
-//                centre of plane q-1, kept from the previous iteration);
-//                slab-halo planes (HALO_LO/HI) are advanced like interior ones.
-//                t_K(p-2K) -> HBM
-//   barrier B
-//   write phase  LDS plane 0 <- in(p); LDS plane s <- t_s(p-2s), s < K;
-//                request in(p+R) (unconditional clamped loads, as in
-//                kernels_temporalk.hip, so the plane wait is a counted vmcnt).
+// Pipeline (as the round-1 kernel: stage s lags stage s-1 by two planes).
+// When plane q of t_{s-1} is "in LDS", stage s
+//     finishes t_s(q-1) = A(q-1) + P9(q)            -> * avg
+//     continues        A(q)  = P9(q-1) + C(q)
+// with A and P9 carried in registers from plane to plane.  What LDS holds of
+// plane q is only its row sums R (the rows y-1, y, y+1: three LDS reads); the
+// lane keeps the plane's values themselves (E from them by DPP lane shifts,
+// and the centre for the ghost cells of intermediate planes).  Per stage and
+// row a lane carries 4 vectors (centre of q and q-1, A, P9; the last stage 3),
+// so 8 waves x 4 rows fit 256 VGPRs.
 //
-// Arithmetic: the leading "0 +" of the reference's sum is folded into
-// fma(sum, avg, +0) exactly as in kernels_temporalk.hip (bit-identical; a
-// -0.0 field is in tests/test_gpu_parity.py).
+// Per step p (one workgroup barrier; the LDS row-sum planes are double-
+// buffered by step parity, so a wave past barrier p has every wave's reads of
+// the buffer it is about to overwrite behind it):
+//   barrier
+//   read phase   for s = 1..K: plane q = p-2s+1 of t_{s-1}: finish t_s(p-2s),
+//                continue A; intermediate planes keep ghost cells at their
+//                input value, slab-halo planes (HALO_LO/HI) are advanced;
+//                t_K(p-2K) -> HBM (nontemporal)
+//   write phase  row sums of in(p) and of t_s(p-2s), s < K, into buffer p&1;
+//                the lane keeps the planes' values; request in(p+2)
+// Bitwise equal to K sweeps of the oracle's box (tests/test_gpu_parity.py).
 #include <cstdlib>
 
 #include "common.hpp"
@@ -43,9 +45,6 @@ template <typename T, int V>
 struct VecB {
     typedef T type __attribute__((ext_vector_type(V)));
 };
-
-__device__ __forceinline__ float bfma0(float s, float a) { return __builtin_fmaf(s, a, 0.0f); }
-__device__ __forceinline__ double bfma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
 
 template <int CTRL>
 __device__ __forceinline__ float bdpp(float v) {
@@ -62,28 +61,24 @@ constexpr int kShr1 = 0x138, kShl1 = 0x130;  // wave_shr:1 / wave_shl:1
 template <typename T, int V, int RY, int NW, int K>
 struct BKTile {
     static constexpr int XR = (K + V - 1) / V;  // ring vectors per x side
-    static constexpr int RW = 64 * V;
-    static constexpr int TX = RW - 2 * XR * V;
-    static constexpr int RH = NW * RY;
-    static constexpr int TY = RH - 2 * K;
-    static constexpr int LX = RW + 2 * V;
-    static constexpr int LY = RH + 2;
-    static constexpr size_t lds_bytes = size_t(K) * LY * LX * sizeof(T);
+    static constexpr int RW = 64 * V;           // region width
+    static constexpr int TX = RW - 2 * XR * V;  // output tile width
+    static constexpr int RH = NW * RY;          // region height
+    static constexpr int TY = RH - 2 * K;       // output tile height
+    static constexpr int LY = RH + 2;           // row-sum planes: one zero pad row each side
+    static constexpr size_t lds_bytes = size_t(2) * K * LY * RW * sizeof(T);
 };
 
-// XD: x-neighbours by DPP lane shifts (true, default) or by two extra LDS
-// reads per row (false; measured 11-13 % slower in fp64 although the DPP
-// moves are ~18 % of the kernel's VALU instructions).
-template <typename T, int V, int RY, int NW, int K, int R, bool XD>
+// Rows: wave w owns region rows w, w + NW, ... (RY of them).
+template <typename T, int V, int RY, int NW, int K>
 __global__ void __launch_bounds__(64 * NW)
-    boxk_27pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int64_t zbeg, int64_t zend, int zchunk,
-              int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg) {
+    box27_sep(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
+              int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
-    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LX = Tl::LX, LY = Tl::LY;
+    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LY = Tl::LY, RW = Tl::RW;
     static_assert(TY > 0 && TX > 0, "tile too small for K");
-    static_assert(R >= 2 && R % 2 == 0, "ring size must be even (register parity)");
-    __shared__ __attribute__((aligned(16))) T L[K][LY][LX];
+    __shared__ __attribute__((aligned(16))) T L[2][K][LY][RW];
 
     const int t = blockIdx.x;
     const int bx = t % tiles_x;
@@ -92,24 +87,24 @@ __global__ void __launch_bounds__(64 * NW)
     const int lane = threadIdx.x, w = threadIdx.y;
     const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
     const int64_t y0 = int64_t(by) * TY - K;
-    // z in 32-bit scalars; addresses = uniform per-plane base + one
-    // non-negative 32-bit byte offset per row (saddr form), as in
-    // kernels_strip.hip
-    const int za = int(zbeg) + bz * zchunk;
-    const int zb = za + zchunk < int(zend) ? za + zchunk : int(zend);
+    const int za = zbeg + bz * zchunk;
+    const int zb = za + zchunk < zend ? za + zchunk : zend;
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
+    // uniform per-plane base + one non-negative 32-bit byte offset per row
+    // (the saddr form of global_load/store, as kernels_strip.hip)
     const int64_t bias = g.row + XR * V;
     const char* __restrict__ src = reinterpret_cast<const char*>(in + g.origin - bias);
     char* __restrict__ dst = reinterpret_cast<char*>(out + g.origin - bias);
 
-    {
-        constexpr int N16 = int(Tl::lds_bytes / 16);
-        VT* l16 = reinterpret_cast<VT*>(&L[0][0][0]);
-        for (int i = threadIdx.y * 64 + threadIdx.x; i < N16; i += 64 * NW) l16[i] = VT{};
+    {  // zero everything once: the pad rows must read as 0 (ring cells only)
+        constexpr int N = int(Tl::lds_bytes / sizeof(VT));
+        VT* l = reinterpret_cast<VT*>(&L[0][0][0][0]);
+        for (int i = threadIdx.y * 64 + threadIdx.x; i < N; i += 64 * NW) l[i] = VT{};
     }
 
-    // unconditional loads from clamped addresses (see kernels_temporalk.hip)
+    // unconditional loads from clamped addresses (the plane wait is a counted
+    // vmcnt, kernels_temporalk.hip)
     uint32_t off[RY];
     bool yin[RY], st[RY];
     const int64_t xmax = g.nx / V * V;
@@ -129,106 +124,90 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
-    const int ld_lo = halo_lo ? -K : -1;
-    const int ld_hi = halo_hi ? nz + K - 1 : nz;
+    const int zfirst = za - K > ld_lo ? za - K : ld_lo;
     const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
     auto load_plane = [&](VT (&d)[RY], int z) {
-        const int zz = z < ld_lo ? ld_lo : (z > zlast ? zlast : z);
+        const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
         for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
     };
 
+    // Registers, per row.  The lane's own values of the stages' input planes
+    // are read in place: in(m) in the input ring vin[(m - p0) % 4] (in(p-2) ..
+    // in(p+1) at step p; loads issued two planes ahead into the slot just
+    // consumed), t_s(m) in H[s-1][(m - p0) & 1] -- no copies, so no load result
+    // is ever moved (a move would wait for the load).  Steps are unrolled 4 at
+    // a time (ring slot and parity are compile-time).
     const int p0 = za - K;
-    VT vin[R][RY];
-    VT part[2][K][RY];  // running sums, parity-indexed: [P^1] = t_s(q-1) (finish), [P] = t_s(q) (continue)
-    VT cen[2][K][RY];   // own centre of the stage's input plane, parity-indexed ([P^1] = plane q-1)
+    VT vin[4][RY];
+    VT H[K > 1 ? K - 1 : 1][2][RY];
+    VT A[K][RY], P9p[K][RY];  // per stage: A(q-1) and P9(q-1)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int k = 0; k < RY; ++k) {
 #pragma unroll
-        for (int s = 0; s < K; ++s)
+        for (int s = 0; s < K; ++s) A[s][k] = P9p[s][k] = VT{};
 #pragma unroll
-            for (int k = 0; k < RY; ++k) {
-                part[b][s][k] = VT{};
-                cen[b][s][k] = VT{};
-            }
+        for (int s = 0; s < (K > 1 ? K - 1 : 1); ++s) H[s][0][k] = H[s][1][k] = VT{};
+        vin[2][k] = vin[3][k] = VT{};
+    }
 #pragma unroll
-    for (int i = 0; i < R; ++i) load_plane(vin[i], p0 + i);
-    const int xx = V + lane * V;
+    for (int i = 0; i < 2; ++i) load_plane(vin[i], p0 + i);
+    __syncthreads();  // LDS zeroed
 
+    // R = (l + c) + r or E = l + r of a row vector v (x-neighbours from the
+    // adjacent lanes)
+    auto row_sum = [&](const VT& v, bool centre) {
+        const T wl = bdpp<kShr1>(v[V - 1]);
+        const T er = bdpp<kShl1>(v[0]);
+        VT o;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
+            const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
+            o[j] = centre ? (l + v[j]) + r : l + r;
+        }
+        return o;
+    };
+
+    const int xl = lane * V;
     auto step = [&](auto S_, int p) {
-        constexpr int S = decltype(S_)::value;
-        constexpr int P = S & 1;
-        __syncthreads();  // A
+        constexpr int S = decltype(S_)::value;  // (p - p0) % 4
+        constexpr int PW = S & 1, PR = PW ^ 1;  // LDS buffer written / read this step
+        __syncthreads();
         VT res[K][RY];
 #pragma unroll
         for (int s = 1; s <= K; ++s) {
-            const int m = p - 2 * s;  // plane finished now
+            const int m = p - 2 * s;  // plane of t_s finished now
             const int lo_s = halo_lo ? -(K - s) : 0;
             const int hi_s = halo_hi ? nz + (K - s) : nz;
             const bool zin = m >= lo_s && m < hi_s;
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
                 const int yy = w + NW * k + 1;
-                // 3 x (V+2) neighbourhood of this lane's cells in plane q
-                T nb[3][V + 2];
-#pragma unroll
-                for (int r = 0; r < 3; ++r) {
-                    const VT c = *reinterpret_cast<const VT*>(&L[s - 1][yy - 1 + r][xx]);
-                    if constexpr (XD) {
-                        nb[r][0] = bdpp<kShr1>(c[V - 1]);
-                    } else {
-                        nb[r][0] = L[s - 1][yy - 1 + r][xx - 1];
-                    }
-#pragma unroll
-                    for (int j = 0; j < V; ++j) nb[r][j + 1] = c[j];
-                    if constexpr (XD) {
-                        nb[r][V + 1] = bdpp<kShl1>(c[0]);
-                    } else {
-                        nb[r][V + 1] = L[s - 1][yy - 1 + r][xx + V];
-                    }
-                }
-                VT fin, cont, start, o;
+                const VT up = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy - 1][xl]);
+                const VT own = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy][xl]);
+                const VT dn = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy + 1][xl]);
+                // plane q = p - 2s + 1 and q - 1 of t_{s-1}: s = 1 -> in(p-1), in(p-2)
+                const VT& cq = s == 1 ? vin[(S + 3) % 4][k] : H[s >= 2 ? s - 2 : 0][(S + 1) & 1][k];
+                const VT& cq1 = s == 1 ? vin[(S + 2) % 4][k] : H[s >= 2 ? s - 2 : 0][S & 1][k];
+                const VT E = row_sum(cq, false);
+                VT o;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
-                    // finish t_s(q-1): + 9 terms (dz = +1)
-                    T a = part[P ^ 1][s - 1][k][j];
-#pragma unroll
-                    for (int r = 0; r < 3; ++r)
-#pragma unroll
-                        for (int dx = 0; dx < 3; ++dx) a += nb[r][j + dx];
-                    fin[j] = a;
-                    // continue t_s(q): + 8 terms (dz = 0, centre skipped)
-                    T b = part[P][s - 1][k][j];
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) b += nb[0][j + dx];
-                    b += nb[1][j];
-                    b += nb[1][j + 2];
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) b += nb[2][j + dx];
-                    cont[j] = b;
-                    // start t_s(q+1): 9 terms (dz = -1); "0 +" folded into the fma
-                    T c0 = nb[0][j] + nb[0][j + 1];
-                    c0 += nb[0][j + 2];
-#pragma unroll
-                    for (int r = 1; r < 3; ++r)
-#pragma unroll
-                        for (int dx = 0; dx < 3; ++dx) c0 += nb[r][j + dx];
-                    start[j] = c0;
-                    o[j] = bfma0(fin[j], avg);
-                    if (s < K) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cen[P ^ 1][s - 1][k][j];
+                    const T p9 = (up[j] + own[j]) + dn[j];
+                    const T c = (up[j] + dn[j]) + E[j];
+                    const T fin = A[s - 1][k][j] + p9;
+                    A[s - 1][k][j] = P9p[s - 1][k][j] + c;
+                    P9p[s - 1][k][j] = p9;
+                    o[j] = fin * avg;
+                    if (s < K) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cq1[j];
                 }
-                part[P ^ 1][s - 1][k] = start;  // t_s(q+1) takes the finished slot
-                part[P][s - 1][k] = cont;
-                VT cc;
-#pragma unroll
-                for (int j = 0; j < V; ++j) cc[j] = nb[1][j + 1];
-                cen[P][s - 1][k] = cc;
                 res[s - 1][k] = o;
-            }
 #ifdef BOXK_SB
-            __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_sched_barrier(0);
 #endif
+            }
         }
         // t_K(p-2K) -> HBM
         const int zo = p - 2 * K;
@@ -248,32 +227,34 @@ __global__ void __launch_bounds__(64 * NW)
                 }
             }
         }
-        __syncthreads();  // B
+        // write phase: row sums of in(p) (stage 1's next input plane) and of
+        // t_s(p-2s) (stage s+1's), s < K
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             const int yy = w + NW * k + 1;
-            *reinterpret_cast<VT*>(&L[0][yy][xx]) = vin[S][k];
 #pragma unroll
-            for (int s = 1; s < K; ++s) *reinterpret_cast<VT*>(&L[s][yy][xx]) = res[s - 1][k];
+            for (int s = 0; s < K; ++s) {
+                // in(p) / t_s(p-2s) -> H[s-1][(p - p0) & 1] (its old content,
+                // t_s(p-2s-2), was stage s+1's plane q-1, read above)
+                if (s > 0) H[s > 0 ? s - 1 : 0][S & 1][k] = res[s > 0 ? s - 1 : 0][k];
+                const VT& v = s == 0 ? vin[S][k] : H[s > 0 ? s - 1 : 0][S & 1][k];
+                *reinterpret_cast<VT*>(&L[PW][s][yy][xl]) = row_sum(v, true);
+            }
         }
-        load_plane(vin[S], p + R);
+        load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
     };
 
     const int plast = zb - 1 + 2 * K;
     int p = p0;
-    for (; p + R - 1 <= plast; p += R) {
+    for (; p + 3 <= plast; p += 4) {
         step(std::integral_constant<int, 0>{}, p);
         step(std::integral_constant<int, 1>{}, p + 1);
-        if constexpr (R > 2) {
-            step(std::integral_constant<int, 2 % R>{}, p + 2);
-            step(std::integral_constant<int, 3 % R>{}, p + 3);
-        }
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
     }
     if (p <= plast) step(std::integral_constant<int, 0>{}, p);
-    if constexpr (R > 2) {
-        if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
-        if (p + 2 <= plast) step(std::integral_constant<int, 2 % R>{}, p + 2);
-    }
+    if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
+    if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
 }
 
 int env_int(const char* name, int dflt) {
@@ -281,7 +262,7 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, int R, bool XD = true>
+template <typename T, int V, int RY, int NW, int K>
 int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
     using Tl = BKTile<T, V, RY, NW, K>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
@@ -289,12 +270,24 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 4 * K >= (int64_t(1) << 30))
-        return set_error(STENCIL_EINVAL, "plane too large for boxk (4 GiB per plane, 2^30 planes)");
+        return set_error(STENCIL_EINVAL, "plane too large for the box kernel (4 GiB per plane, 2^30 planes)");
+    const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
+    if (K > 1 && (lo || hi) && l.zghost < K)
+        return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
+                         (long long)l.zghost);
+    // planes the launch may read: the ghost / halo planes its range needs
+    // (single sweeps may cover slab-halo planes themselves: stencil_sweep)
+    const int64_t ld_lo = std::min<int64_t>(lo ? -K : -1, begin - 1);
+    const int64_t ld_hi = std::max<int64_t>(hi ? g.nz + K - 1 : g.nz, end);
+    if (ld_lo < -l.zghost || ld_hi > g.nz + l.zghost - 1)
+        return set_error(STENCIL_EINVAL, "box sweep of planes [%lld, %lld) reads past the %lld ghost planes",
+                         (long long)begin, (long long)end, (long long)l.zghost);
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = boxk_27pt<T, V, RY, NW, K, R, XD>;
+    auto kern = box27_sep<T, V, RY, NW, K>;
     int zc = env_int("STENCIL_BOXK_ZCHUNK", 0);
     if (zc <= 0) {
-        // as kernels_temporalk.hip, with the 3K-plane pipeline fill of this kernel
+        // chunk count c minimising rounds x (chunk + 3K): a chunk's march
+        // costs its planes plus the 3K-plane pipeline fill (kernels_strip.hip)
         int slots = 0;
         if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
         const int64_t tiles = gx * gy;
@@ -309,71 +302,75 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     }
     const int64_t gz = (nz + zc - 1) / zc;
     const int64_t nb = gx * gy * gz;
-    if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for boxk");
-    const bool lo = l.prob.flags & STENCIL_HALO_LO, hi = l.prob.flags & STENCIL_HALO_HI;
-    if ((lo || hi) && l.zghost < K)
-        return set_error(STENCIL_EINVAL, "%d fused steps across a slab halo need halo >= %d (got %lld)", K, K,
-                         (long long)l.zghost);
+    if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
-                       static_cast<T*>(out), g, begin, end, zc, int(gx), int(gy), int(lo), int(hi),
-                       avg_weight<T>(l.prob));
+                       static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
+                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
 
 }  // namespace
 
+bool box27_supports(const stencil_problem& p) {
+    return p.dims == 3 && p.shape == STENCIL_BOX && p.radius == 1 && p.order == STENCIL_ORDER_NAIVE;
+}
+
+// Workgroup shape cfg = RY*100 + NW (rows per wave x waves), STENCIL_BOXK_CFG.
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                 hipStream_t s) {
     if (!box27_supports(l.prob))
-        return set_error(STENCIL_EUNSUPPORTED, "BOXK supports the 3D r=1 naive 27-point box only");
-    // cfg = RY*100 + NW
+        return set_error(STENCIL_EUNSUPPORTED, "the box kernel supports the 3D r=1 naive 27-point box only");
     const int cfg = env_int("STENCIL_BOXK_CFG", 0);
     if (l.prob.dtype == STENCIL_F32) {
-        if (steps == 2) {
+        switch (steps) {
+        case 1:
+            return launch_bk<float, 4, 2, 16, 1>(l, in, out, begin, end, s);
+        case 2:
             switch (cfg) {
-            case 408: return launch_bk<float, 4, 4, 8, 2, 2>(l, in, out, begin, end, s);
-            case 208: return launch_bk<float, 4, 2, 8, 2, 2>(l, in, out, begin, end, s);
-            case 116: return launch_bk<float, 4, 1, 16, 2, 2>(l, in, out, begin, end, s);
-            case 1116: return launch_bk<float, 2, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
-            case 1416: return launch_bk<float, 4, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
-            case 1216: return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
-            default:
-                // measured (tools/box_ab.sh): 16-B lanes with LDS x-neighbours
-                // on wide rows (2048^2 x 256: 735 vs 685 Gcell/s), 8-B lanes
-                // with DPP on narrow ones (512^3: 582 vs 504)
-                if (l.prob.nx >= 1024) return launch_bk<float, 4, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
-                return launch_bk<float, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            case 216: return launch_bk<float, 4, 2, 16, 2>(l, in, out, begin, end, s);
+            case 408: return launch_bk<float, 4, 4, 8, 2>(l, in, out, begin, end, s);
+            case 208: return launch_bk<float, 4, 2, 8, 2>(l, in, out, begin, end, s);
+            case 20116: return launch_bk<float, 2, 1, 16, 2>(l, in, out, begin, end, s);
+            default: return launch_bk<float, 4, 1, 16, 2>(l, in, out, begin, end, s);
             }
-        }
-        if (steps == 3) {
+        case 3:
             switch (cfg) {
-            case 208: return launch_bk<float, 4, 2, 8, 3, 2>(l, in, out, begin, end, s);
-            default: return launch_bk<float, 4, 1, 16, 3, 2>(l, in, out, begin, end, s);
+            case 208: return launch_bk<float, 4, 2, 8, 3>(l, in, out, begin, end, s);
+            default: return launch_bk<float, 4, 1, 16, 3>(l, in, out, begin, end, s);
             }
+        default: break;
         }
     } else {
-        if (steps == 2) {
+        switch (steps) {
+        case 1:
+            return launch_bk<double, 2, 2, 16, 1>(l, in, out, begin, end, s);
+        case 2:
             switch (cfg) {
-            case 216: return launch_bk<double, 2, 2, 16, 2, 2>(l, in, out, begin, end, s);
-            case 308: return launch_bk<double, 2, 3, 8, 2, 2>(l, in, out, begin, end, s);
-            case 408: return launch_bk<double, 2, 4, 8, 2, 2>(l, in, out, begin, end, s);
-            case 212: return launch_bk<double, 2, 2, 12, 2, 2>(l, in, out, begin, end, s);
-            case 208: return launch_bk<double, 2, 2, 8, 2, 2>(l, in, out, begin, end, s);
-            case 1116: return launch_bk<double, 2, 1, 16, 2, 2, false>(l, in, out, begin, end, s);
-            default: return launch_bk<double, 2, 1, 16, 2, 2>(l, in, out, begin, end, s);
+            case 216: return launch_bk<double, 2, 2, 16, 2>(l, in, out, begin, end, s);
+            case 408: return launch_bk<double, 2, 4, 8, 2>(l, in, out, begin, end, s);
+            case 308: return launch_bk<double, 2, 3, 8, 2>(l, in, out, begin, end, s);
+            case 208: return launch_bk<double, 2, 2, 8, 2>(l, in, out, begin, end, s);
+            case 10116: return launch_bk<double, 1, 1, 16, 2>(l, in, out, begin, end, s);
+            case 10216: return launch_bk<double, 1, 2, 16, 2>(l, in, out, begin, end, s);
+            default: return launch_bk<double, 2, 1, 16, 2>(l, in, out, begin, end, s);
             }
-        }
-        if (steps == 3) {
+        case 3:
             switch (cfg) {
-            case 208: return launch_bk<double, 2, 2, 8, 3, 2>(l, in, out, begin, end, s);
-            case 308: return launch_bk<double, 2, 3, 8, 3, 2>(l, in, out, begin, end, s);
-            case 408: return launch_bk<double, 2, 4, 8, 3, 2>(l, in, out, begin, end, s);
-            default: return launch_bk<double, 2, 1, 16, 3, 2>(l, in, out, begin, end, s);
+            case 308: return launch_bk<double, 2, 3, 8, 3>(l, in, out, begin, end, s);
+            case 208: return launch_bk<double, 2, 2, 8, 3>(l, in, out, begin, end, s);
+            default: return launch_bk<double, 2, 1, 16, 3>(l, in, out, begin, end, s);
             }
+        default: break;
         }
     }
-    return set_error(STENCIL_EINVAL, "boxk steps must be 2 or 3 (got %d)", steps);
+    return set_error(STENCIL_EINVAL, "box kernel steps must be 1, 2 or 3 (got %d)", steps);
+}
+
+// Single sweeps and fused pairs of the box (stencil_sweep / stencil_sweep2).
+int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                 hipStream_t s) {
+    return launch_boxk(l, in, out, begin, end, steps, s);
 }
 
 }  // namespace stencil

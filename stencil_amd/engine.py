@@ -257,3 +257,78 @@ def copy_bandwidth(nbytes: int, reps: int = 20, device: int = 0) -> float:
     _lib.check(lib.stencil_copy_bandwidth(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
                                           nbytes, reps, _stream_handle(None), ctypes.byref(ms)), "copy")
     return 2.0 * nbytes * reps / (ms.value * 1e-3) / 1e9
+
+
+class SlabJob:
+    """A multi-GPU z-slab job run by the C++ host (stencil_slab_*, csrc/slab.hip):
+    one process, `devices` one slab each, halos over RCCL (or device copies,
+    which let several slabs share a GPU).  The counterpart of slab.py's
+    per-process driver for callers without torch.distributed."""
+
+    def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int, devices, exchange: str = "rccl",
+                 periodic: bool = False):
+        self.lib = _lib.load()
+        self.spec = spec
+        self.shape = (nx, ny, nz)
+        prob = spec.problem(nx, ny, nz)
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        job = ctypes.c_void_p()
+        kind = _lib.EXCHANGE_RCCL if exchange == "rccl" else _lib.EXCHANGE_COPY
+        _lib.check(self.lib.stencil_slab_create(ctypes.byref(prob), len(devices), devs, kind,
+                                                _lib.SLAB_PERIODIC if periodic else 0, ctypes.byref(job)),
+                   "stencil_slab_create")
+        self.job = job
+        self.nslabs = len(devices)
+
+    def close(self) -> None:
+        if self.job:
+            self.lib.stencil_slab_destroy(self.job)
+            self.job = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self, slab: int) -> dict:
+        first, planes = ctypes.c_int64(0), ctypes.c_int64(0)
+        dev, k = ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_slab_info(self.job, slab, ctypes.byref(first), ctypes.byref(planes),
+                                              ctypes.byref(dev), ctypes.byref(k)), "stencil_slab_info")
+        return {"first": int(first.value), "planes": int(planes.value), "device": int(dev.value),
+                "sweeps_per_round": int(k.value)}
+
+    def fill_initial(self, kind: str = "reference", seed: int = 0) -> None:
+        k = _lib.INIT_RANDOM if kind == "random" else _lib.INIT_REFERENCE
+        _lib.check(self.lib.stencil_slab_fill_initial(self.job, k, seed), "stencil_slab_fill_initial")
+
+    def _dense(self) -> np.ndarray:
+        nx, ny, nz = self.shape
+        r = self.spec.radius
+        dt = np.float64 if self.spec.dtype == "fp64" else np.float32
+        return np.zeros((nz + 2 * r, ny + 2 * r, nx + 2 * r), dtype=dt)
+
+    def upload(self, dense: np.ndarray) -> None:
+        a = np.ascontiguousarray(dense)
+        _lib.check(self.lib.stencil_slab_upload(self.job, ctypes.c_void_p(a.ctypes.data), a.shape[2], a.shape[1]),
+                   "stencil_slab_upload")
+
+    def download(self) -> np.ndarray:
+        """The current global grid, dense with ghosts (oracle layout)."""
+        a = self._dense()
+        _lib.check(self.lib.stencil_slab_download(self.job, ctypes.c_void_p(a.ctypes.data), a.shape[2], a.shape[1]),
+                   "stencil_slab_download")
+        return a
+
+    def run(self, iterations: int) -> float:
+        """`iterations` sweeps; returns the host wall time of the rounds (ms)."""
+        ms = ctypes.c_float(0.0)
+        _lib.check(self.lib.stencil_slab_run(self.job, iterations, ctypes.byref(ms)), "stencil_slab_run")
+        return float(ms.value)
+
+    def plane_sums(self) -> np.ndarray:
+        out = np.zeros(self.shape[2], dtype=np.float64)
+        _lib.check(self.lib.stencil_slab_plane_sums(self.job, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+                   "stencil_slab_plane_sums")
+        return out

@@ -41,6 +41,10 @@ def test_extensions():
     assert (c["dims"], c["nz"], c["dtype"], c["kernel"], c["shape"]) == ("3", "512", "fp64", "zmarch", "star")
     c = cfg("-s", "16", "-b", "1", "-i", "2", "-m", "HIP", "--points", "27", "--nx", "20", "--nz", "3")
     assert (c["dims"], c["shape"], c["nx"], c["ny"], c["nz"]) == ("3", "box", "20", "16", "3")
+    c = cfg("-s", "16", "-b", "1", "-i", "2", "-m", "HIPMultiGPU", "--points", "7", "--gpus", "8")
+    assert (c["gpus"], c["exchange"], c["methods"]) == ("8", "rccl", "HIPMultiGPU")
+    c = cfg("-s", "16", "-b", "1", "-i", "2", "-m", "HIP", "--gpus=3", "--exchange", "copy", "--share-device")
+    assert (c["gpus"], c["exchange"]) == ("3", "copy")
 
 
 @pytest.mark.parametrize("args", [
@@ -53,6 +57,8 @@ def test_extensions():
     ["-s", "64", "-b", "8", "-i", "3", "-m"],                # -m needs a value
     ["-s", "64", "-b", "8", "-i", "3", "-m", "DMA", "stray", "--dims", "4"],
     ["--help"],                                             # parse() returns nullopt after help
+    ["-s", "64", "-b", "8", "-i", "3", "-m", "HIP", "--gpus", "0"],
+    ["-s", "64", "-b", "8", "-i", "3", "-m", "HIP", "--exchange", "mpi"],
 ])
 def test_parse_failures_exit_1(args):
     p = run(*args)

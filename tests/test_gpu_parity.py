@@ -316,13 +316,14 @@ def test_tkstrip_packed_schedule_small_shapes(gpu, dtype):
     assert any(packed), list(zip(shapes, packed))
 
 
-@pytest.mark.parametrize("cfg", ["default", "308", "216", "1116", "208", "116", "1416", "1216"])
+@pytest.mark.parametrize("cfg", ["default", "216", "408", "308", "208", "10116", "10216", "20116"])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 def test_boxk_chunking(gpu, monkeypatch, cfg, zchunk, dtype):
-    """27-point box, two fused sweeps per launch through the K-step box kernel
-    (kernels_boxk.hip): workgroup shapes (incl. spilling ones), forced z-chunks
-    shorter and longer than the 3K-plane pipeline fill, odd iteration counts."""
+    """27-point box, two fused sweeps per launch through the separable-sum box
+    kernel (kernels_boxk.hip): workgroup shapes (incl. spilling ones), forced
+    z-chunks shorter and longer than the 3K-plane pipeline fill, odd iteration
+    counts (the remainder single sweep is the same kernel with K = 1)."""
     monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
     if cfg != "default":
         monkeypatch.setenv("STENCIL_BOXK_CFG", cfg)
@@ -374,14 +375,29 @@ def test_temporalk_signed_zero_field(gpu, shape, steps, dtype):
     assert same_bits(np.ascontiguousarray(got), np.ascontiguousarray(a))
 
 
-@pytest.mark.parametrize("cfg", ["0"])
-def test_box_fused_shapes(gpu, monkeypatch, cfg):
-    monkeypatch.setenv("STENCIL_BOX_CFG", cfg)
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("zchunk", ["0", "3", "8"])
+def test_box_single_sweeps(gpu, monkeypatch, dtype, zchunk):
+    """The box's single sweep (the K = 1 instance of kernels_boxk.hip) over the
+    whole grid and over sub-ranges of planes."""
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
     nx, ny, nz = 150, 47, 21
-    p = ob.problem(3, "fp64", "box", 1, "naive", nx, ny, nz)
-    want = ob.run(p, 4, "random", 3)
-    _, got = gpu_run(gpu, 3, "fp64", "box", 1, "naive", "temporal2", nx, ny, nz, 4, "random", 3)
-    assert same_bits(got, want)
+    p = ob.problem(3, dtype, "box", 1, "naive", nx, ny, nz)
+    for it in (1, 3):
+        want = ob.run(p, it, "random", 3)
+        _, got = gpu_run(gpu, 3, dtype, "box", 1, "naive", "zmarch", nx, ny, nz, it, "random", 3)
+        assert same_bits(got, want), it
+    e = engine(gpu, 3, dtype, "box", 1, "naive", "zmarch", nx, ny, nz)
+    e.reset("random", 9)
+    import torch
+    ref = e.to_numpy(e.a).copy()
+    e.sweep(e.a, e.b, 4, 13)
+    torch.cuda.synchronize()
+    a = ref.copy()
+    b = ref.copy()
+    ob.sweep(p, a, b, 4, 13)
+    got = e.to_numpy(e.b)
+    assert same_bits(got[4 + 1:13 + 1], b[4 + 1:13 + 1])
 
 
 def test_sweep2_subrange(gpu):
@@ -603,6 +619,27 @@ def test_cli_check_result_on_gpu(gpu):
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr + out.stdout
     assert out.stdout.count("is correct.") == 2
+
+
+def test_cli_multi_gpu_slabs(gpu):
+    """The drop-in runs a z-slab job from the C++ host: HIPMultiGPU over one
+    GPU through RCCL, and 3 / 4 slabs sharing the GPU with device-copy halos
+    (RCCL refuses two ranks on one GPU) -- each checked against the CPU naive
+    sweep with -c, the reference's stdout lines intact."""
+    import re
+    cli = os.path.join(ROOT, "build", "bin", "stencil_main")
+    base = [cli, "-s", "40", "-b", "1", "-i", "13", "--dims", "3", "--nz", "37", "--init", "random", "-c"]
+    runs = [base + ["-m", "HIPMultiGPU", "--dtype", "fp64"],
+            base + ["-m", "HIPMultiGPU", "HIP", "--gpus", "3", "--share-device", "--exchange", "copy"],
+            base + ["-m", "HIP", "--gpus", "4", "--share-device", "--exchange", "copy", "--points", "27",
+                    "--dtype", "fp64"]]
+    for args in runs:
+        out = subprocess.run(args, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr + out.stdout
+        for m in set(args[args.index("-m") + 1:][:2]) & {"HIPMultiGPU", "HIP"}:
+            assert f"The results of method {m} is correct." in out.stdout
+            assert re.search(rf"The average time taken by {m} method is [0-9.e+-]+ms for 13 iterations\.",
+                             out.stdout)
 
 
 def test_cli_block_reach(gpu):
