@@ -49,7 +49,8 @@ PRESETS = {
     "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=2,
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
     "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
-               desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, 2-step temporal blocking"),
+               desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, temporal blocking (3 sweeps per launch, "
+                    "deeper than the config's 2; bitwise the same result)"),
     # north_star's 4096^3 fp64 needs 2 x 550 GB; its largest single-GPU
     # proxy is 2048^3 fp64: 2 x 70 GB with ghosts and padding
     "NS": dict(dtype="fp64", shape="star", grid=(2048, 2048, 2048), min_gpus=1,

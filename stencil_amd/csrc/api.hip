@@ -141,6 +141,19 @@ int iterate_tk_steps(const stencil_problem& p) {
     return steps >= 3 && steps <= 5 ? steps : 0;
 }
 
+// Sweeps per launch of the 27-point box in stencil_iterate (AUTO, or explicit
+// TEMPORALK): K = 3 launches of kernels_boxk.hip, remainder as a pair / single
+// (STENCIL_BOX_STEPS=2: pairs only).  Measured (tools/box_k3_ab.sh,
+// profiles/r02e_ab_box_k3.log): 2048^2 x 256 fp64 717 vs 651 Gcell/s for pairs,
+// fp32 1242 vs 1182; 512^3 equal.  0 = not used.
+int iterate_box_steps(const stencil_problem& p) {
+    if (!box27_supports(p)) return 0;
+    if (!(p.kernel == STENCIL_KERNEL_TEMPORALK || (p.kernel == STENCIL_KERNEL_AUTO && iterate_fused(p)))) return 0;
+    const char* k = std::getenv("STENCIL_BOX_STEPS");
+    const int steps = k && *k ? std::atoi(k) : 3;
+    return steps == 3 ? 3 : 0;
+}
+
 // 2D problems iterate K sweeps per launch with the tile resident in LDS
 // (kernels_tb2d.hip) unless a single-sweep family is forced.
 bool iterate_tb2d(const stencil_problem& p) {
@@ -590,7 +603,8 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
         return STENCIL_OK;
     }
     const bool t2 = !iterate_tb2d(l->prob) && iterate_fused(l->prob);
-    const int64_t k = iterate_tk_steps(l->prob);
+    const int64_t kb = iterate_box_steps(l->prob);
+    const int64_t k = kb ? kb : iterate_tk_steps(l->prob);
     int64_t n = iterations;
     if (k) {
         const int64_t r = n % k;
@@ -599,7 +613,7 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
         n = n / 2 + n % 2;
     }
     if (launches) *launches = n;
-    if (kernel) *kernel = k ? STENCIL_KERNEL_TEMPORALK : t2 ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
+    if (kernel) *kernel = (k && !kb) ? STENCIL_KERNEL_TEMPORALK : t2 || kb ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
     return STENCIL_OK;
 }
 
@@ -652,6 +666,12 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
     if (const uint32_t k = uint32_t(iterate_tk_steps(l->prob))) {
         for (; i + k <= iterations && rc == STENCIL_OK; i += k) {
             rc = launch_temporalk(*l, in, out, 0, n, int(k), s);
+            std::swap(in, out);
+        }
+    }
+    if (const uint32_t k = uint32_t(iterate_box_steps(l->prob))) {
+        for (; i + k <= iterations && rc == STENCIL_OK; i += k) {
+            rc = launch_boxk(*l, in, out, 0, n, int(k), s);
             std::swap(in, out);
         }
     }

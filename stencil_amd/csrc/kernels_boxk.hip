@@ -337,7 +337,12 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         case 3:
             switch (cfg) {
             case 208: return launch_bk<float, 4, 2, 8, 3>(l, in, out, begin, end, s);
-            default: return launch_bk<float, 4, 1, 16, 3>(l, in, out, begin, end, s);
+            case 20116: return launch_bk<float, 2, 1, 16, 3>(l, in, out, begin, end, s);
+            case 20216: return launch_bk<float, 2, 2, 16, 3>(l, in, out, begin, end, s);
+            case 416: return launch_bk<float, 4, 1, 16, 3>(l, in, out, begin, end, s);
+            // 8-B lanes, 3 rows x 8 waves: 2048^2 x 256 1242 vs 315 Gcell/s for
+            // 16-B lanes x 16 waves (spills), profiles/r02e_ab_box_k3.log
+            default: return launch_bk<float, 2, 3, 8, 3>(l, in, out, begin, end, s);
             }
         default: break;
         }
@@ -359,7 +364,14 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             switch (cfg) {
             case 308: return launch_bk<double, 2, 3, 8, 3>(l, in, out, begin, end, s);
             case 208: return launch_bk<double, 2, 2, 8, 3>(l, in, out, begin, end, s);
-            default: return launch_bk<double, 2, 1, 16, 3>(l, in, out, begin, end, s);
+            case 10116: return launch_bk<double, 1, 1, 16, 3>(l, in, out, begin, end, s);
+            case 10216: return launch_bk<double, 1, 2, 16, 3>(l, in, out, begin, end, s);
+            case 10308: return launch_bk<double, 1, 3, 8, 3>(l, in, out, begin, end, s);
+            case 10408: return launch_bk<double, 1, 4, 8, 3>(l, in, out, begin, end, s);
+            case 216: return launch_bk<double, 2, 1, 16, 3>(l, in, out, begin, end, s);
+            // one cell per lane, 3 rows x 8 waves: 2048^2 x 256 717 vs 190 Gcell/s
+            // for 2 cells x 16 waves (spills), profiles/r02e_ab_box_k3.log
+            default: return launch_bk<double, 1, 3, 8, 3>(l, in, out, begin, end, s);
             }
         default: break;
         }

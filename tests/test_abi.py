@@ -132,7 +132,11 @@ def test_plan_counts_launches(monkeypatch):
     assert launches.value == 7 and kernel.value == _lib.KERNEL_ZMARCH
     lay = _lib.make_layout(_lib.make_problem(dims=3, shape=_lib.BOX, nx=8, ny=8, nz=8))
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
-    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # 27-point: 2-step BOXK pairs + single
+    assert launches.value == 3 and kernel.value == _lib.KERNEL_TEMPORAL2  # 27-point: 2 x 3-step launches + single
+    monkeypatch.setenv("STENCIL_BOX_STEPS", "2")
+    assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 4 and kernel.value == _lib.KERNEL_TEMPORAL2  # pairs + single
+    monkeypatch.delenv("STENCIL_BOX_STEPS")
     lay = _lib.make_layout(_lib.make_problem(dims=3, radius=2, nx=8, ny=8, nz=8))
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_DIRECT

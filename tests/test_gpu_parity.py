@@ -337,8 +337,15 @@ def test_boxk_chunking(gpu, monkeypatch, cfg, zchunk, dtype):
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (7, 5, 3), (250, 19, 12)])
-def test_boxk_three_steps(gpu, dtype, shape3):
-    """stencil_sweepk(3) on the 27-point box equals three plain sweeps."""
+@pytest.mark.parametrize("cfg", ["default", "10116", "216", "20116", "416", "208"])
+@pytest.mark.parametrize("zchunk", ["0", "5"])
+def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
+    """stencil_sweepk(3) on the 27-point box (AUTO's box launch) equals three
+    plain sweeps, every workgroup shape, forced short z-chunks; and a whole
+    job through AUTO (3-sweep launches + remainder pair / single)."""
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_BOXK_CFG", cfg)
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
     nx, ny, nz = shape3
     p = ob.problem(3, dtype, "box", 1, "naive", nx, ny, nz)
     want = ob.run(p, 3, "random", 5)
@@ -346,6 +353,11 @@ def test_boxk_three_steps(gpu, dtype, shape3):
     e.reset("random", 5)
     e.sweepk(e.a, e.b, 0, nz, 3)
     assert same_bits(e.to_numpy(e.b), want)
+    for it in (7, 8):
+        e.reset("random", 5)
+        fin, _ = e.iterate(it)
+        assert same_bits(e.to_numpy(fin), ob.run(p, it, "random", 5)), it
+    assert e.plan(8) == (3, 3)
 
 
 @pytest.mark.parametrize("shape,steps", [("star", 3), ("star", 4), ("box", 2), ("box", 3)])

@@ -35,7 +35,7 @@ def test_slab_job_copy_equals_single_grid(gpu, dtype, shape_name, nslabs):
     shape = (70, 45, 41)
     job = SlabJob(spec, *shape, devices=[gpu] * nslabs, exchange="copy")
     k = job.info(0)["sweeps_per_round"]
-    assert k == (2 if shape_name == "box" else 4)
+    assert k == (3 if shape_name == "box" else 4)
     assert sum(job.info(i)["planes"] for i in range(nslabs)) == shape[2]
     job.fill_initial("random", 12)
     it = 3 * k + 1
