@@ -523,8 +523,11 @@ int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, in
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
     int nsig = 0;
-    const int rc = launch_tkstrip_signal(*l, in, out, begin, end, steps, counters,
-                                         reinterpret_cast<unsigned long long*>(face_signal), &nsig, as_stream(stream));
+    auto* fsig = reinterpret_cast<unsigned long long*>(face_signal);
+    const int rc = box27_supports(l->prob)
+                       ? launch_boxk_signal(*l, in, out, begin, end, steps, counters, fsig, &nsig, as_stream(stream))
+                       : launch_tkstrip_signal(*l, in, out, begin, end, steps, counters, fsig, &nsig,
+                                               as_stream(stream));
     if (rc == STENCIL_OK) {
         if (signals_per_face) *signals_per_face = nsig;
         clear_error();

@@ -95,6 +95,8 @@ int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, in
                           unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s);
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                 hipStream_t s);
+int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                       unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s);
 bool zmarch_supports(const stencil_problem& p);
 bool temporal2_supports(const stencil_problem& p);
 int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

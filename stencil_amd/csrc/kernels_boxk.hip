@@ -70,10 +70,18 @@ struct BKTile {
 };
 
 // Rows: wave w owns region rows w, w + NW, ... (RY of them).
-template <typename T, int V, int RY, int NW, int K>
+// SIG: face signalling for multi-GPU slabs (stencil_sweepk_signal, as
+// kernels_strip.hip): the last z-chunk of every tile marches DOWNWARD, so the
+// K planes of both faces are among the first stored, and the workgroup that
+// stores a face adds to sig[0] / sig[1] (release, then one agent-scope add).
+// Marching down, plane z's sum ((P9(z-1) + C(z)) + P9(z+1)) needs the NEWEST
+// plane sum first, so the down-march carries C(z) and the two previous plane
+// sums instead of the pre-added A: same additions, same order, bitwise equal.
+template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_sep(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
-              int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg) {
+              int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
+              unsigned long long* __restrict__ fsig) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LY = Tl::LY, RW = Tl::RW;
@@ -89,6 +97,8 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t y0 = int64_t(by) * TY - K;
     const int za = zbeg + bz * zchunk;
     const int zb = za + zchunk < zend ? za + zchunk : zend;
+    const int nch = (zend - zbeg + zchunk - 1) / zchunk;
+    const bool rev = SIG && nch >= 2 && bz == nch - 1;  // this workgroup's chunk marches down
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
     // uniform per-plane base + one non-negative 32-bit byte offset per row
@@ -124,9 +134,31 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
+    // R = (l + c) + r or E = l + r of a row vector v (x-neighbours from the
+    // adjacent lanes)
+    auto row_sum = [&](const VT& v, bool centre) {
+        const T wl = bdpp<kShr1>(v[V - 1]);
+        const T er = bdpp<kShl1>(v[0]);
+        VT o;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
+            const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
+            o[j] = centre ? (l + v[j]) + r : l + r;
+        }
+        return o;
+    };
+    const int xl = lane * V;
+    __syncthreads();  // LDS zeroed
+
+    auto segment = [&](auto REV_) {  // the chunk [za, zb), marched up or (REV) down
+    constexpr bool REV = decltype(REV_)::value;
     const int zfirst = za - K > ld_lo ? za - K : ld_lo;
     const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
-    auto load_plane = [&](VT (&d)[RY], int z) {
+    // march index m -> plane
+    auto zr = [&](int m) { return REV ? za + zb - 1 - m : m; };
+    auto load_plane = [&](VT (&d)[RY], int m) {
+        const int z = zr(m);
         const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
@@ -142,35 +174,22 @@ __global__ void __launch_bounds__(64 * NW)
     const int p0 = za - K;
     VT vin[4][RY];
     VT H[K > 1 ? K - 1 : 1][2][RY];
-    VT A[K][RY], P9p[K][RY];  // per stage: A(q-1) and P9(q-1)
+    // per stage, carried from plane to plane: up-march A(q-1) and P9(q-1);
+    // down-march (REV) C(q-1), P9(q-1), P9(q-2) (march order)
+    VT A[K][RY], P9p[K][RY], P9q[REV ? K : 1][RY];
 #pragma unroll
     for (int k = 0; k < RY; ++k) {
 #pragma unroll
         for (int s = 0; s < K; ++s) A[s][k] = P9p[s][k] = VT{};
+#pragma unroll
+        for (int s = 0; s < (REV ? K : 1); ++s) P9q[s][k] = VT{};
 #pragma unroll
         for (int s = 0; s < (K > 1 ? K - 1 : 1); ++s) H[s][0][k] = H[s][1][k] = VT{};
         vin[2][k] = vin[3][k] = VT{};
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) load_plane(vin[i], p0 + i);
-    __syncthreads();  // LDS zeroed
 
-    // R = (l + c) + r or E = l + r of a row vector v (x-neighbours from the
-    // adjacent lanes)
-    auto row_sum = [&](const VT& v, bool centre) {
-        const T wl = bdpp<kShr1>(v[V - 1]);
-        const T er = bdpp<kShl1>(v[0]);
-        VT o;
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
-            const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
-            o[j] = centre ? (l + v[j]) + r : l + r;
-        }
-        return o;
-    };
-
-    const int xl = lane * V;
     auto step = [&](auto S_, int p) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % 4
         constexpr int PW = S & 1, PR = PW ^ 1;  // LDS buffer written / read this step
@@ -178,7 +197,7 @@ __global__ void __launch_bounds__(64 * NW)
         VT res[K][RY];
 #pragma unroll
         for (int s = 1; s <= K; ++s) {
-            const int m = p - 2 * s;  // plane of t_s finished now
+            const int m = zr(p - 2 * s);  // plane of t_s finished now
             const int lo_s = halo_lo ? -(K - s) : 0;
             const int hi_s = halo_hi ? nz + (K - s) : nz;
             const bool zin = m >= lo_s && m < hi_s;
@@ -197,9 +216,17 @@ __global__ void __launch_bounds__(64 * NW)
                 for (int j = 0; j < V; ++j) {
                     const T p9 = (up[j] + own[j]) + dn[j];
                     const T c = (up[j] + dn[j]) + E[j];
-                    const T fin = A[s - 1][k][j] + p9;
-                    A[s - 1][k][j] = P9p[s - 1][k][j] + c;
-                    P9p[s - 1][k][j] = p9;
+                    T fin;
+                    if constexpr (!REV) {
+                        fin = A[s - 1][k][j] + p9;  // (P9(q-2) + C(q-1)) + P9(q)
+                        A[s - 1][k][j] = P9p[s - 1][k][j] + c;
+                        P9p[s - 1][k][j] = p9;
+                    } else {  // plane zr(q-1): (P9(zr(q)) + C(zr(q-1))) + P9(zr(q-2))
+                        fin = (p9 + A[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j];
+                        A[s - 1][k][j] = c;
+                        P9q[REV ? s - 1 : 0][k][j] = P9p[s - 1][k][j];
+                        P9p[s - 1][k][j] = p9;
+                    }
                     o[j] = fin * avg;
                     if (s < K) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cq1[j];
                 }
@@ -212,7 +239,7 @@ __global__ void __launch_bounds__(64 * NW)
         // t_K(p-2K) -> HBM
         const int zo = p - 2 * K;
         if (zo >= za && zo < zb) {
-            char* obase = dst + int64_t(zo) * plane * int64_t(sizeof(T));
+            char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
                 if (st[k]) {
@@ -223,6 +250,34 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
                         for (int j = 0; j < V; ++j)
                             if (xst[j]) q[j] = res[K - 1][k][j];
+                    }
+                }
+            }
+        }
+        if constexpr (SIG) {
+            // right after the store of a face's last plane (every chunk is at
+            // least K planes): the low face is [zbeg, zbeg+K) of the first
+            // chunk, the high face [zend-K, zend) of the last, walked down
+            // (REV) so it comes first -- as kernels_strip.hip
+            const bool lo_here = !REV && za == zbeg && zo == za + K - 1;
+            const bool hi_here = zb == zend && zo == (REV ? za + K - 1 : zb - 1);
+            if (lo_here || hi_here) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0 && threadIdx.y == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const unsigned ntiles = unsigned(tiles_x) * unsigned(tiles_y);
+                    bool last = false;
+                    if (lo_here)
+                        last |= (__hip_atomic_fetch_add(&sig[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (hi_here)
+                        last |= (__hip_atomic_fetch_add(&sig[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (fsig && last) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __hip_atomic_fetch_add(fsig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
             }
@@ -255,6 +310,13 @@ __global__ void __launch_bounds__(64 * NW)
     if (p <= plast) step(std::integral_constant<int, 0>{}, p);
     if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
     if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
+    };  // segment
+    if constexpr (SIG) {
+        if (rev) segment(std::true_type{});
+        else segment(std::false_type{});
+    } else {
+        segment(std::false_type{});
+    }
 }
 
 int env_int(const char* name, int dflt) {
@@ -262,8 +324,9 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K>
-int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s) {
+template <typename T, int V, int RY, int NW, int K, bool SIG = false>
+int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
+              unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = BKTile<T, V, RY, NW, K>;
     static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
@@ -283,14 +346,14 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         return set_error(STENCIL_EINVAL, "box sweep of planes [%lld, %lld) reads past the %lld ghost planes",
                          (long long)begin, (long long)end, (long long)l.zghost);
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = box27_sep<T, V, RY, NW, K>;
+    const int64_t tiles = gx * gy;
+    auto kern = box27_sep<T, V, RY, NW, K, SIG>;
     int zc = env_int("STENCIL_BOXK_ZCHUNK", 0);
     if (zc <= 0) {
         // chunk count c minimising rounds x (chunk + 3K): a chunk's march
         // costs its planes plus the 3K-plane pipeline fill (kernels_strip.hip)
         int slots = 0;
         if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
-        const int64_t tiles = gx * gy;
         int64_t best_c = 1, best = INT64_MAX;
         for (int64_t c = 1; c <= nz; ++c) {
             const int64_t z = (nz + c - 1) / c;
@@ -298,14 +361,32 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
             const int64_t cost = ((tiles * c + slots - 1) / slots) * (z + 3 * K);
             if (cost <= best) best = cost, best_c = c;
         }
+        if (SIG) {
+            // face-signalled slab rounds: the most chunks that fit ONE round
+            // with a CU per XCD to spare (the exchange runs beside the launch,
+            // kernels_strip.hip)
+            const int64_t room = slots - slots / 32;
+            for (int64_t c = 1; tiles * c <= room && c <= nz; ++c) {
+                if (c > 1 && (nz + c - 1) / c < 3 * K) break;
+                best_c = c;
+            }
+        }
         zc = int((nz + best_c - 1) / best_c);
     }
+    if constexpr (SIG) {
+        // every chunk at least K planes (a face lies inside one chunk)
+        int64_t nch = (nz + zc - 1) / zc;
+        auto last = [&](int64_t c) { return nz - (c - 1) * ((nz + c - 1) / c); };
+        while (nch > 1 && ((nz + nch - 1) / nch < K || last(nch) < K)) --nch;
+        zc = int((nz + nch - 1) / nch);
+        if (nsig) *nsig = int(tiles);
+    }
     const int64_t gz = (nz + zc - 1) / zc;
-    const int64_t nb = gx * gy * gz;
+    const int64_t nb = tiles * gz;
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob));
+                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
@@ -377,6 +458,38 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         }
     }
     return set_error(STENCIL_EINVAL, "box kernel steps must be 1, 2 or 3 (got %d)", steps);
+}
+
+// Face-signalled box launches for multi-GPU slab rounds (stencil_sweepk_signal):
+// the default shapes of launch_boxk.
+int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                       unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s) {
+    if (!box27_supports(l.prob))
+        return set_error(STENCIL_EUNSUPPORTED, "the box kernel supports the 3D r=1 naive 27-point box only");
+    const int cfg = env_int("STENCIL_BOXK_SIG_CFG", 0);
+    if (l.prob.dtype == STENCIL_F32) {
+        switch (steps) {
+        case 2: return launch_bk<float, 4, 1, 16, 2, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 3:
+            if (cfg == 20308) return launch_bk<float, 2, 3, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            if (cfg == 20208) return launch_bk<float, 2, 2, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            return launch_bk<float, 2, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        default: break;
+        }
+    } else {
+        switch (steps) {
+        case 2: return launch_bk<double, 2, 1, 16, 2, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 3:
+            // 1 row x 16 waves: the down-march's extra carried sum makes the
+            // 3-row shape spill (33 VGPRs); 2048^3 interior rank 685 vs 607
+            // Gcell/s (profiles/r02h_bench_c5_loopback_sig*.json)
+            if (cfg == 10308) return launch_bk<double, 1, 3, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            if (cfg == 10208) return launch_bk<double, 1, 2, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            return launch_bk<double, 1, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        default: break;
+        }
+    }
+    return set_error(STENCIL_EINVAL, "face-signalled box sweeps: steps must be 2 or 3 (got %d)", steps);
 }
 
 // Single sweeps and fused pairs of the box (stencil_sweep / stencil_sweep2).

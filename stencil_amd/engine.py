@@ -127,10 +127,12 @@ class JacobiEngine:
 
     @property
     def supports_signal(self) -> bool:
-        """Face-signalled K-step launches (stencil_sweepk_signal): 3D 7-point star."""
+        """Face-signalled K-step launches (stencil_sweepk_signal): the 3D 7-point
+        star (K = 3..5) and the 27-point box (K = 2, 3)."""
         s = self.spec
-        return (s.dims == 3 and s.shape == "star" and s.radius == 1 and s.order == "naive" and self.fused
-                and 3 <= self.fuse_steps <= 5)
+        if not (s.dims == 3 and s.radius == 1 and s.order == "naive" and self.fused):
+            return False
+        return 3 <= self.fuse_steps <= 5 if s.shape == "star" else 2 <= self.fuse_steps <= 3
 
     def sweepk_signal(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int,
                       counters: torch.Tensor, stream=None, face_signal: "FaceSignal | None" = None) -> int:

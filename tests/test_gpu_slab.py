@@ -197,6 +197,33 @@ def test_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, fla
     assert sig[0].item() == nsig and sig[1].item() == nsig and sig[2].item() == 0 and nsig > 0
 
 
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("steps", [2, 3])
+@pytest.mark.parametrize("zchunk", ["0", "5", "9", "40"])
+@pytest.mark.parametrize("flags", [0, 3])
+@pytest.mark.parametrize("cfg", ["0", "10308", "20308", "10208"])
+def test_box_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, flags, cfg):
+    """The 27-point box's face-signalled launch (kernels_boxk.hip SIG: the last
+    z-chunk marches down, carrying C and two plane sums instead of the
+    pre-added A) is bitwise stencil_sweepk, one counter add per tile and face."""
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
+    monkeypatch.setenv("STENCIL_BOXK_SIG_CFG", cfg)
+    nx, ny, nz = 77, 51, 31
+    spec = StencilSpec(dims=3, dtype=dtype, shape="box", halo=3)
+    e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=flags)
+    e.reset("random", 9)
+    ref = torch.empty_like(e.b)
+    ref.copy_(e.b)
+    e.sweepk(e.a, ref, 0, nz, steps)
+    sig = torch.zeros(4, dtype=torch.int32, device=e.a.device)
+    nsig = e.sweepk_signal(e.a, e.b, 0, nz, steps, sig)
+    e.wait_counters(sig, nsig, nsig)
+    torch.cuda.synchronize()
+    ib = torch.int64 if dtype == "fp64" else torch.int32
+    assert torch.equal(e.b.view(ib), ref.view(ib))
+    assert sig[0].item() == nsig and sig[1].item() == nsig and sig[2].item() == 0 and nsig > 0
+
+
 @pytest.mark.parametrize("dtype,steps", [("fp64", 4), ("fp32", 4), ("fp64", 3), ("fp32", 5)])
 def test_face_signal_counts_completed_faces(gpu, dtype, steps):
     """The face signal (HIP signal memory, waited on by the command processor)
@@ -232,11 +259,11 @@ def test_face_signal_counts_completed_faces(gpu, dtype, steps):
     fs.close()
 
 
-def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=True, dtype="fp64"):
+def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=True, dtype="fp64", shape="star"):
     from stencil_amd.slab import SlabInfo, SlabJacobi
-    spec = StencilSpec(dims=3, dtype=dtype)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
     fuse = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
-    spec = StencilSpec(dims=3, dtype=dtype, halo=max(2, fuse))
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape, halo=max(2, fuse))
     e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
     SlabJacobi.use_signal = signalled
     default_fs = SlabJacobi.use_face_signal
@@ -302,6 +329,21 @@ def test_signalled_rounds_then_remainder_large_plane(gpu, dtype):
     nz, it = 2 * fuse, 2 * fuse + 2  # two signalled rounds + a remainder pair
     want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype)
     got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, False, dtype=dtype)
+    ib = torch.int64 if dtype == "fp64" else torch.int32
+    assert torch.equal(got.view(ib), want.view(ib))
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("shape3,it", [((70, 45, 33), 13), ((130, 64, 20), 9), ((64, 7, 6), 8), ((64, 7, 9), 10)])
+@pytest.mark.parametrize("face_signal", [True, False])
+def test_box_signalled_rounds_match_boundary_launches(gpu, dtype, shape3, it, face_signal):
+    """27-point box slab rounds as one face-signalled launch (K = 3, the box's
+    fuse depth) give bit for bit the boundary + interior rounds, with
+    remainders after the K-rounds and the minimum slab (nz = 2K)."""
+    from stencil_amd.slab import LoopbackExchanger
+    nx, ny, nz = shape3
+    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype, shape="box")
+    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, face_signal, dtype=dtype, shape="box")
     ib = torch.int64 if dtype == "fp64" else torch.int32
     assert torch.equal(got.view(ib), want.view(ib))
 
