@@ -38,6 +38,13 @@
 
 #include "common.hpp"
 
+#ifndef BOXS_OPAQUE
+#define BOXS_OPAQUE 0
+#endif
+#ifndef BOXS_SB
+#define BOXS_SB 0
+#endif
+
 namespace stencil {
 namespace {
 
@@ -297,6 +304,275 @@ __global__ void __launch_bounds__(64 * NW)
             }
         }
         load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
+#if BOXS_SB >= 1
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    };
+
+    const int plast = zb - 1 + 2 * K;
+    int p = p0;
+    for (; p + 3 <= plast; p += 4) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    if (p <= plast) step(std::integral_constant<int, 0>{}, p);
+    if (p + 1 <= plast) step(std::integral_constant<int, 1>{}, p + 1);
+    if (p + 2 <= plast) step(std::integral_constant<int, 2>{}, p + 2);
+    };  // segment
+    if constexpr (SIG) {
+        if (rev) segment(std::true_type{});
+        else segment(std::false_type{});
+    } else {
+        segment(std::false_type{});
+    }
+}
+
+// The STRIP layout of the same pipeline (kernels_strip.hip did this for the
+// 7-point star): wave w owns CONSECUTIVE region rows [w*RY, w*RY + RY), so a
+// row's y-neighbour row sums come from the lane's own registers and only the
+// strip's first and last row sums go through LDS (2 writes + 2 reads per
+// stage and wave instead of RY writes + 3*RY reads).  The freed LDS traffic
+// and the res[K][RY] staging of box27_sep (stages now run K .. 1, so stage s
+// writes t_s straight into the history slot stage s+1 has just read) pay for
+// taller regions: 8 waves x 6 rows = 48 rows for 42 output rows (y over-fetch
+// 1.14) instead of 24 for 18 (1.33).  Same sums, same order, same pipeline
+// (stage s lags two planes per stage), bitwise equal to box27_sep.
+//
+// Per step p (one barrier; boundary row sums double-buffered by step parity):
+//   barrier
+//   stage K     plane q = p-2K+1 of t_{K-1}: finish t_K(p-2K) -> HBM
+//   stage s<K   finish t_s(p-2s) into H[s-1] (the slot stage s+1 read),
+//               its first / last row sums -> LDS buffer p&1
+//   row sums of in(p)'s first / last rows -> LDS buffer p&1; request in(p+2)
+template <typename T, int V, int RY, int NW, int K, bool SIG = false>
+__global__ void __launch_bounds__(64 * NW)
+    box27_strip(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
+                int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
+                unsigned long long* __restrict__ fsig) {
+    using Tl = BKTile<T, V, RY, NW, K>;
+    using VT = typename VecB<T, V>::type;
+    constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW;
+    static_assert(TY > 0 && TX > 0, "tile too small for K");
+    static_assert(RY >= 2, "a strip needs a first and a last row");
+    // boundary row sums: [step parity][stage input][wave][first, last row][RW]
+    __shared__ __attribute__((aligned(16))) T L[2][K][NW][2][RW];
+
+    const int t = blockIdx.x;
+    const int bx = t % tiles_x;
+    const int by = (t / tiles_x) % tiles_y;
+    const int bz = t / (tiles_x * tiles_y);
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
+    const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
+    const int za = zbeg + bz * zchunk;
+    const int zb = za + zchunk < zend ? za + zchunk : zend;
+    const int nch = (zend - zbeg + zchunk - 1) / zchunk;
+    const bool rev = SIG && nch >= 2 && bz == nch - 1;  // this workgroup's chunk marches down
+    const int nz = int(g.nz);
+    const int64_t plane = g.plane;
+    const int64_t bias = g.row + XR * V;
+    const char* __restrict__ src = reinterpret_cast<const char*>(in + g.origin - bias);
+    char* __restrict__ dst = reinterpret_cast<char*>(out + g.origin - bias);
+
+    {  // the first step reads a buffer nobody wrote (ring cells only): zero it
+        constexpr int N = int(sizeof(L) / sizeof(VT));
+        VT* l = reinterpret_cast<VT*>(&L[0][0][0][0][0]);
+        for (int i = threadIdx.y * 64 + threadIdx.x; i < N; i += 64 * NW) l[i] = VT{};
+    }
+
+    uint32_t off[RY];
+    bool yin[RY], st[RY];
+    const int64_t xmax = g.nx / V * V;
+    const int64_t xc = x < xmax ? x : xmax;
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const int rr = w * RY + k;
+        const int64_t y = y0 + k;
+        const int64_t yc = y < -1 ? -1 : (y > g.ny ? g.ny : y);
+        off[k] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
+        yin[k] = y >= 0 && y < g.ny;
+        st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < 64 - XR;
+    }
+    bool xin[V], xst[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        xin[j] = x + j >= 0 && x + j < g.nx;
+        xst[j] = x + j < g.nx;
+    }
+    // R = (l + c) + r and E = l + r of a row vector (x-neighbours by DPP)
+    auto sums = [&](const VT& v, VT& R, VT& E) {
+#if BOXS_SB >= 4
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        const T wl = bdpp<kShr1>(v[V - 1]);
+        const T er = bdpp<kShl1>(v[0]);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
+            const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
+            E[j] = l + r;
+            R[j] = (l + v[j]) + r;
+        }
+    };
+    auto rsum = [&](const VT& v) {
+        VT R, E;
+        sums(v, R, E);
+        return R;
+    };
+    const int xl = lane * V;
+    // neighbour strips (the first / last wave reads its own: ring rows)
+    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+    __syncthreads();  // LDS zeroed
+
+    auto segment = [&](auto REV_) {
+    constexpr bool REV = decltype(REV_)::value;
+    const int zfirst = za - K > ld_lo ? za - K : ld_lo;
+    const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
+    auto zr = [&](int m) { return REV ? za + zb - 1 - m : m; };
+    auto load_plane = [&](VT (&d)[RY], int m) {
+        const int z = zr(m);
+        const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
+        const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
+#if BOXS_OPAQUE
+        asm volatile("" : "+s"(base));  // keep base + 32-bit offset (saddr form)
+#endif
+#pragma unroll
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
+    };
+
+    // in(m) in vin[(m - p0) % 4], t_s(m) in H[s-1][(m - p0) & 1] (read in
+    // place); per stage the carried A(q-1) / P9(q-1) (REV: C, P9(q-1), P9(q-2))
+    const int p0 = za - K;
+    VT vin[4][RY];
+    VT H[K > 1 ? K - 1 : 1][2][RY];
+    VT A[K][RY], P9p[K][RY], P9q[REV ? K : 1][RY];
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+#pragma unroll
+        for (int s = 0; s < K; ++s) A[s][k] = P9p[s][k] = VT{};
+#pragma unroll
+        for (int s = 0; s < (REV ? K : 1); ++s) P9q[s][k] = VT{};
+#pragma unroll
+        for (int s = 0; s < (K > 1 ? K - 1 : 1); ++s) H[s][0][k] = H[s][1][k] = VT{};
+        vin[2][k] = vin[3][k] = VT{};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) load_plane(vin[i], p0 + i);
+
+    auto step = [&](auto S_, int p) {
+        constexpr int S = decltype(S_)::value;  // (p - p0) % 4
+        constexpr int PW = S & 1, PR = PW ^ 1;  // LDS buffer written / read this step
+        __syncthreads();
+        const int zo = p - 2 * K;  // t_K(zo) -> HBM this step
+        const bool do_store = zo >= za && zo < zb;
+        char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
+#if BOXS_OPAQUE
+        asm volatile("" : "+s"(obase));
+#endif
+        auto stage = [&](auto s_) {
+            constexpr int s = decltype(s_)::value;
+            const int m = zr(p - 2 * s);  // plane of t_s finished now
+            const int lo_s = halo_lo ? -(K - s) : 0;
+            const int hi_s = halo_hi ? nz + (K - s) : nz;
+            const bool zin = m >= lo_s && m < hi_s;
+            // rows of plane q = p - 2s + 1 (centre) and q - 1 of t_{s-1}
+            auto cq = [&](int k) -> const VT& { return s == 1 ? vin[(S + 3) % 4][k] : H[s >= 2 ? s - 2 : 0][(S + 1) & 1][k]; };
+            auto cq1 = [&](int k) -> const VT& { return s == 1 ? vin[(S + 2) % 4][k] : H[s >= 2 ? s - 2 : 0][S & 1][k]; };
+            VT Rm = *reinterpret_cast<const VT*>(&L[PR][s - 1][wa][1][xl]);  // row above the strip
+            VT Rc, Ec;
+            sums(cq(0), Rc, Ec);
+#pragma unroll
+            for (int k = 0; k < RY; ++k) {
+                VT Rn, En{};
+                if (k == RY - 1) Rn = *reinterpret_cast<const VT*>(&L[PR][s - 1][wb][0][xl]);  // row below
+                else sums(cq(k + 1 < RY ? k + 1 : k), Rn, En);
+                VT o;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const T p9 = (Rm[j] + Rc[j]) + Rn[j];
+                    const T c = (Rm[j] + Rn[j]) + Ec[j];
+                    T fin;
+                    if constexpr (!REV) {
+                        fin = A[s - 1][k][j] + p9;  // (P9(q-2) + C(q-1)) + P9(q)
+                        A[s - 1][k][j] = P9p[s - 1][k][j] + c;
+                        P9p[s - 1][k][j] = p9;
+                    } else {  // plane zr(q-1): (P9(zr(q)) + C(zr(q-1))) + P9(zr(q-2))
+                        fin = (p9 + A[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j];
+                        A[s - 1][k][j] = c;
+                        P9q[REV ? s - 1 : 0][k][j] = P9p[s - 1][k][j];
+                        P9p[s - 1][k][j] = p9;
+                    }
+                    o[j] = fin * avg;
+                    if (s < K) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cq1(k)[j];
+                }
+                if constexpr (s == K) {
+                    if (do_store && st[k]) {
+                        T* qp = reinterpret_cast<T*>(obase + off[k]);
+                        if (xst[V - 1]) {
+                            __builtin_nontemporal_store(o, reinterpret_cast<VT*>(qp));
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < V; ++j)
+                                if (xst[j]) qp[j] = o[j];
+                        }
+                    }
+                } else {
+                    // t_s(p-2s) takes the slot of t_s(p-2s-2), stage s+1's
+                    // plane q-1, already read (stages run K .. 1)
+                    H[s < K ? s - 1 : 0][S & 1][k] = o;
+                    if (k == 0) *reinterpret_cast<VT*>(&L[PW][s][w][0][xl]) = rsum(o);
+                    if (k == RY - 1) *reinterpret_cast<VT*>(&L[PW][s][w][1][xl]) = rsum(o);
+                }
+                Rm = Rc;
+                Rc = Rn;
+                Ec = En;
+#if BOXS_SB >= 3
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+            }
+#if BOXS_SB >= 2
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        };
+        stage(std::integral_constant<int, K>{});
+        if constexpr (SIG) {
+            // right after the store of a face's last plane (box27_sep)
+            const bool lo_here = !REV && za == zbeg && zo == za + K - 1;
+            const bool hi_here = zb == zend && zo == (REV ? za + K - 1 : zb - 1);
+            if (lo_here || hi_here) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0 && threadIdx.y == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const unsigned ntiles = unsigned(tiles_x) * unsigned(tiles_y);
+                    bool last = false;
+                    if (lo_here)
+                        last |= (__hip_atomic_fetch_add(&sig[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (hi_here)
+                        last |= (__hip_atomic_fetch_add(&sig[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                                    ntiles == 0;
+                    if (fsig && last) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        __hip_atomic_fetch_add(fsig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+            }
+        }
+        if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? K - 1 : 1)>{});
+        if constexpr (K >= 3) stage(std::integral_constant<int, 1>{});
+        if constexpr (K == 2) stage(std::integral_constant<int, 1>{});
+        static_assert(K >= 1 && K <= 3, "K = 1..3");
+        // stage 1's next input plane: in(p)
+        *reinterpret_cast<VT*>(&L[PW][0][w][0][xl]) = rsum(vin[S][0]);
+        *reinterpret_cast<VT*>(&L[PW][0][w][1][xl]) = rsum(vin[S][RY - 1]);
+        load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
+#if BOXS_SB >= 1
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     };
 
     const int plast = zb - 1 + 2 * K;
@@ -324,11 +600,11 @@ int env_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-template <typename T, int V, int RY, int NW, int K, bool SIG = false>
+template <typename T, int V, int RY, int NW, int K, bool SIG = false, bool STRIP = false>
 int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = BKTile<T, V, RY, NW, K>;
-    static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
+    static_assert((STRIP ? size_t(2) * K * NW * 2 * Tl::RW * sizeof(T) : Tl::lds_bytes) <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
@@ -347,7 +623,10 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
                          (long long)begin, (long long)end, (long long)l.zghost);
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
     const int64_t tiles = gx * gy;
-    auto kern = box27_sep<T, V, RY, NW, K, SIG>;
+    auto kern = [] {
+        if constexpr (STRIP) return box27_strip<T, V, RY, NW, K, SIG>;
+        else return box27_sep<T, V, RY, NW, K, SIG>;
+    }();
     int zc = env_int("STENCIL_BOXK_ZCHUNK", 0);
     if (zc <= 0) {
         // chunk count c minimising rounds x (chunk + 3K): a chunk's march
@@ -403,6 +682,35 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
     if (!box27_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "the box kernel supports the 3D r=1 naive 27-point box only");
     const int cfg = env_int("STENCIL_BOXK_CFG", 0);
+    // strip layout (box27_strip): cfg = 9VRRNN (V cells per lane, RR rows per wave, NN waves)
+    if (cfg >= 900000) {
+        if (l.prob.dtype == STENCIL_F32) {
+            switch (steps * 1000000 + cfg) {
+            case 3920408: return launch_bk<float, 2, 4, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 3920312: return launch_bk<float, 2, 3, 12, 3, false, true>(l, in, out, begin, end, s);
+            case 2920408: return launch_bk<float, 2, 4, 8, 2, false, true>(l, in, out, begin, end, s);
+            case 2920312: return launch_bk<float, 2, 3, 12, 2, false, true>(l, in, out, begin, end, s);
+            case 2940208: return launch_bk<float, 4, 2, 8, 2, false, true>(l, in, out, begin, end, s);
+            case 3920216: return launch_bk<float, 2, 2, 16, 3, false, true>(l, in, out, begin, end, s);
+            case 1940408: return launch_bk<float, 4, 4, 8, 1, false, true>(l, in, out, begin, end, s);
+            default: break;
+            }
+        } else {
+            switch (steps * 1000000 + cfg) {
+            case 3910408: return launch_bk<double, 1, 4, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 3910312: return launch_bk<double, 1, 3, 12, 3, false, true>(l, in, out, begin, end, s);
+            case 3910212: return launch_bk<double, 1, 2, 12, 3, false, true>(l, in, out, begin, end, s);
+            case 3910308: return launch_bk<double, 1, 3, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 2910408: return launch_bk<double, 1, 4, 8, 2, false, true>(l, in, out, begin, end, s);
+            case 2910312: return launch_bk<double, 1, 3, 12, 2, false, true>(l, in, out, begin, end, s);
+            case 2910216: return launch_bk<double, 1, 2, 16, 2, false, true>(l, in, out, begin, end, s);
+            case 3910216: return launch_bk<double, 1, 2, 16, 3, false, true>(l, in, out, begin, end, s);
+            case 1920408: return launch_bk<double, 2, 4, 8, 1, false, true>(l, in, out, begin, end, s);
+            default: break;
+            }
+        }
+        // no strip shape for this (dtype, steps): the default shapes below
+    }
     if (l.prob.dtype == STENCIL_F32) {
         switch (steps) {
         case 1:
@@ -421,9 +729,11 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 20116: return launch_bk<float, 2, 1, 16, 3>(l, in, out, begin, end, s);
             case 20216: return launch_bk<float, 2, 2, 16, 3>(l, in, out, begin, end, s);
             case 416: return launch_bk<float, 4, 1, 16, 3>(l, in, out, begin, end, s);
-            // 8-B lanes, 3 rows x 8 waves: 2048^2 x 256 1242 vs 315 Gcell/s for
-            // 16-B lanes x 16 waves (spills), profiles/r02e_ab_box_k3.log
-            default: return launch_bk<float, 2, 3, 8, 3>(l, in, out, begin, end, s);
+            case 20308: return launch_bk<float, 2, 3, 8, 3>(l, in, out, begin, end, s);
+            // strip layout, 8-B lanes, 4 rows x 8 waves: 2048^2 x 256 1504 vs 1012,
+            // 512^3 1349 vs 879, 2048^3 1510 vs 1116 Gcell/s for the interleaved
+            // 3 x 8 (profiles/r02j_ab_box_strip.log)
+            default: return launch_bk<float, 2, 4, 8, 3, false, true>(l, in, out, begin, end, s);
             }
         default: break;
         }
@@ -450,9 +760,14 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 10308: return launch_bk<double, 1, 3, 8, 3>(l, in, out, begin, end, s);
             case 10408: return launch_bk<double, 1, 4, 8, 3>(l, in, out, begin, end, s);
             case 216: return launch_bk<double, 2, 1, 16, 3>(l, in, out, begin, end, s);
-            // one cell per lane, 3 rows x 8 waves: 2048^2 x 256 717 vs 190 Gcell/s
-            // for 2 cells x 16 waves (spills), profiles/r02e_ab_box_k3.log
-            default: return launch_bk<double, 1, 3, 8, 3>(l, in, out, begin, end, s);
+            // strip layout, one cell per lane (profiles/r02j_ab_box_strip.log):
+            // planes of < 1024^2 cells 4 rows x 8 waves (512^3 773 vs 578 Gcell/s
+            // for the interleaved 3 x 8), larger planes 2 rows x 16 waves
+            // (2048^2 x 256 759 vs 706, 2048^3 766 vs 739; 4 x 8 loses there)
+            default:
+                if (l.prob.nx * l.prob.ny < (int64_t(1) << 20))
+                    return launch_bk<double, 1, 4, 8, 3, false, true>(l, in, out, begin, end, s);
+                return launch_bk<double, 1, 2, 16, 3, false, true>(l, in, out, begin, end, s);
             }
         default: break;
         }
@@ -467,25 +782,43 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
     if (!box27_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "the box kernel supports the 3D r=1 naive 27-point box only");
     const int cfg = env_int("STENCIL_BOXK_SIG_CFG", 0);
+    if (cfg >= 900000) {  // strip layout, as launch_boxk
+        if (l.prob.dtype == STENCIL_F32) {
+            switch (steps * 1000000 + cfg) {
+            case 3920408: return launch_bk<float, 2, 4, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 3920308: return launch_bk<float, 2, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            default: break;
+            }
+        } else {
+            switch (steps * 1000000 + cfg) {
+            case 3910408: return launch_bk<double, 1, 4, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 3910308: return launch_bk<double, 1, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 3910312: return launch_bk<double, 1, 3, 12, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            default: break;
+            }
+        }
+    }
     if (l.prob.dtype == STENCIL_F32) {
         switch (steps) {
         case 2: return launch_bk<float, 4, 1, 16, 2, true>(l, in, out, begin, end, s, sig, nsig, fsig);
         case 3:
             if (cfg == 20308) return launch_bk<float, 2, 3, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             if (cfg == 20208) return launch_bk<float, 2, 2, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-            return launch_bk<float, 2, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            if (cfg == 20116) return launch_bk<float, 2, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            // strip layout, 3 rows x 8 waves (4 rows spill with the down-march's carry)
+            return launch_bk<float, 2, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
         default: break;
         }
     } else {
         switch (steps) {
         case 2: return launch_bk<double, 2, 1, 16, 2, true>(l, in, out, begin, end, s, sig, nsig, fsig);
         case 3:
-            // 1 row x 16 waves: the down-march's extra carried sum makes the
-            // 3-row shape spill (33 VGPRs); 2048^3 interior rank 685 vs 607
-            // Gcell/s (profiles/r02h_bench_c5_loopback_sig*.json)
             if (cfg == 10308) return launch_bk<double, 1, 3, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             if (cfg == 10208) return launch_bk<double, 1, 2, 8, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-            return launch_bk<double, 1, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            if (cfg == 10116) return launch_bk<double, 1, 1, 16, 3, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            // strip layout, 3 rows x 8 waves: 2048^3 interior rank 758 vs 659
+            // Gcell/s for the interleaved 1 x 16 (profiles/r02k_bench_c5_loopback_sig*.json)
+            return launch_bk<double, 1, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
         default: break;
         }
     }

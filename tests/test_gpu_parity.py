@@ -360,6 +360,32 @@ def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
     assert e.plan(8) == (3, 3)
 
 
+BOX_STRIP_CFGS = {"fp64": {3: ["910408", "910308", "910312", "910212", "910216"], 2: ["910408", "910312", "910216"],
+                            1: ["920408"]},
+                   "fp32": {3: ["920408", "920312", "920216"], 2: ["920408", "920312", "940208"], 1: ["940408"]}}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("steps", [1, 2, 3])
+@pytest.mark.parametrize("shape3", [(131, 61, 29), (7, 5, 3), (250, 119, 12), (64, 300, 40)])
+@pytest.mark.parametrize("zchunk", ["0", "5", "13"])
+def test_box_strip_shapes(gpu, monkeypatch, dtype, steps, shape3, zchunk):
+    """The strip layout of the box kernel (box27_strip: consecutive rows per
+    wave, only the strips' first / last row sums through LDS), every shape
+    instantiated for the step count: stencil_sweepk(K) bitwise equal to K
+    sweeps of the oracle, ragged tiles, forced short z-chunks."""
+    monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
+    nx, ny, nz = shape3
+    p = ob.problem(3, dtype, "box", 1, "naive", nx, ny, nz)
+    want = ob.run(p, steps, "random", 17)
+    for cfg in BOX_STRIP_CFGS[dtype][steps]:
+        monkeypatch.setenv("STENCIL_BOXK_CFG", cfg)
+        e = engine(gpu, 3, dtype, "box", 1, "naive", "auto", nx, ny, nz)
+        e.reset("random", 17)
+        e.sweepk(e.a, e.b, 0, nz, steps)
+        assert same_bits(e.to_numpy(e.b), want), cfg
+
+
 @pytest.mark.parametrize("shape,steps", [("star", 3), ("star", 4), ("box", 2), ("box", 3)])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 def test_temporalk_signed_zero_field(gpu, shape, steps, dtype):

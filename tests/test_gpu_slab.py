@@ -201,7 +201,7 @@ def test_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, fla
 @pytest.mark.parametrize("steps", [2, 3])
 @pytest.mark.parametrize("zchunk", ["0", "5", "9", "40"])
 @pytest.mark.parametrize("flags", [0, 3])
-@pytest.mark.parametrize("cfg", ["0", "10308", "20308", "10208"])
+@pytest.mark.parametrize("cfg", ["0", "10308", "20308", "10208", "10116", "20116", "910408", "910312", "920408"])
 def test_box_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, flags, cfg):
     """The 27-point box's face-signalled launch (kernels_boxk.hip SIG: the last
     z-chunk marches down, carrying C and two plane sums instead of the
