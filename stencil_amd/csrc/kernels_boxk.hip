@@ -48,6 +48,16 @@
 namespace stencil {
 namespace {
 
+// A per-row 32-bit offset made opaque at each use: the zero extension then
+// sits next to the address add in the loop body, so instruction selection
+// forms saddr + 32-bit voffset (global_load v, voff, s[base]) instead of a
+// 64-bit VGPR address built by v_lshl_add_u64 from a hoisted zext (2 VGPRs
+// per row held across the loop, one VALU op per access).
+__device__ __forceinline__ uint32_t row_off(uint32_t o) {
+    asm volatile("" : "+v"(o));
+    return o;
+}
+
 template <typename T, int V>
 struct VecB {
     typedef T type __attribute__((ext_vector_type(V)));
@@ -169,7 +179,7 @@ __global__ void __launch_bounds__(64 * NW)
         const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
-        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + row_off(off[k]));
     };
 
     // Registers, per row.  The lane's own values of the stages' input planes
@@ -250,7 +260,7 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
                 if (st[k]) {
-                    T* q = reinterpret_cast<T*>(obase + off[k]);
+                    T* q = reinterpret_cast<T*>(obase + row_off(off[k]));
                     if (xst[V - 1]) {
                         __builtin_nontemporal_store(res[K - 1][k], reinterpret_cast<VT*>(q));
                     } else {
@@ -439,7 +449,7 @@ __global__ void __launch_bounds__(64 * NW)
         asm volatile("" : "+s"(base));  // keep base + 32-bit offset (saddr form)
 #endif
 #pragma unroll
-        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + row_off(off[k]));
     };
 
     // in(m) in vin[(m - p0) % 4], t_s(m) in H[s-1][(m - p0) & 1] (read in
@@ -509,7 +519,7 @@ __global__ void __launch_bounds__(64 * NW)
                 }
                 if constexpr (s == K) {
                     if (do_store && st[k]) {
-                        T* qp = reinterpret_cast<T*>(obase + off[k]);
+                        T* qp = reinterpret_cast<T*>(obase + row_off(off[k]));
                         if (xst[V - 1]) {
                             __builtin_nontemporal_store(o, reinterpret_cast<VT*>(qp));
                         } else {

@@ -47,6 +47,10 @@
 
 #include "common.hpp"
 
+#ifndef TK_FAST_PATH
+#define TK_FAST_PATH 1
+#endif
+
 namespace stencil {
 namespace {
 
@@ -114,11 +118,11 @@ struct StripTile {
 // (hipStreamWaitValue64) with no wait kernel resident during the launch.
 // NS: input planes in registers -- in(p-2) .. in(p+NS-3): loads are issued
 // NS-2 planes ahead (4: two planes).
-template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4>
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -206,12 +210,20 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
+    // the whole region inside the grid in x and y: intermediate stages need no
+    // ghost-cell select on steps whose stage planes are all inside in z
+    const bool xy_inner = fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
+                          int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny;
     const int ld_lo = halo_lo ? -K : -1;
     const int ld_hi = halo_hi ? nz + K - 1 : nz;
     const int zfirst = za - K > ld_lo ? za - K : ld_lo;
     const int zlast = zb + K - 1 < ld_hi ? zb + K - 1 : ld_hi;
     // march index m -> plane: the chunk is walked upward, or downward (REV)
     auto zr = [&](int m) { return REV ? za + zb - 1 - m : m; };
+    // (the box kernels make each use of off[k] opaque to get the saddr +
+    // 32-bit voffset form; here that costs the fp64 fast-path shape its
+    // register fit -- 9 spilled VGPRs, 910 vs 1212 Gcell/s at 512^3 -- so the
+    // hoisted 64-bit offsets stay, profiles/r02p_ab_saddr_fast.log)
     auto load_plane = [&](VT (&d)[RY], int m) {
         const int z = zr(m);
         const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
@@ -239,8 +251,9 @@ __global__ void __launch_bounds__(64 * NW)
     for (int i = 0; i < NS - 2; ++i) load_plane(vin[i], p0 + i);
 
 
-    auto step = [&](auto S_, int p) {
+    auto stepb = [&](auto S_, int p, auto FAST_) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % LCM
+        constexpr bool FAST = decltype(FAST_)::value;  // no ghost-cell selects this step
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
         constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
         __syncthreads();  // boundary rows of step p-1 are visible
@@ -296,7 +309,7 @@ __global__ void __launch_bounds__(64 * NW)
                     sum += REV ? zp[j] : zm[j];
                     sum += REV ? zm[j] : zp[j];
                     o[j] = DIAG == 2 ? c[j] : sfma0(sum, avg);
-                    if (s < K) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
+                    if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
                 }
                 // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
                 if constexpr (s >= 2) H[s - 2][(S - s + 5) & 1][k] = prev;
@@ -361,6 +374,23 @@ __global__ void __launch_bounds__(64 * NW)
             }
         }
         if constexpr (DIAG != 1) load_plane(vin[(S + NS - 2) % NS], p + NS - 2);  // slot of in(p-2), consumed above
+    };
+    auto step = [&](auto S_, int p) {
+        // compiled for the fp64 one-cell-per-lane shapes only: duplicating the
+        // step costs the fp32 / signalled shapes their register fit
+        constexpr bool kFast = TK_FAST_PATH && FP && sizeof(T) == 8 && V == 1 && !SIG && DIAG == 0;
+        if constexpr (!kFast) {
+            stepb(S_, p, std::false_type{});
+            return;
+        }
+        bool all_in = xy_inner;
+#pragma unroll
+        for (int s = 1; s < K; ++s) {
+            const int z = zr(p - s);
+            all_in = all_in && z >= (halo_lo ? -(K - s) : 0) && z < (halo_hi ? nz + (K - s) : nz);
+        }
+        if (all_in) stepb(S_, p, std::true_type{});
+        else stepb(S_, p, std::false_type{});
     };
 
     const int plast = zb + K - 1;
@@ -470,7 +500,8 @@ int packed_schedule(int dev, int64_t tiles, int64_t nz, int K, int slots, int zc
     return STENCIL_OK;
 }
 
-template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4>
+template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
+          bool FP = true>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
@@ -481,7 +512,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS>;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP>;
     const int64_t tiles = gx * gy;
     int dev = 0, slots = 0;
     STENCIL_HIP_CHECK(hipGetDevice(&dev));
@@ -549,6 +580,11 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (rc != STENCIL_OK) return rc;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
+    // interior steps without ghost-cell selects (fp64 one-cell-per-lane shapes):
+    // by default only where the packed schedule runs -- few tiles, 512^3 fp64
+    // 1212 vs 1175 Gcell/s -- since on large planes the duplicated step loses
+    // (2048^2 x 512 1357 vs 1384, 2048^3 1310 vs 1365; profiles/r02o_ab_tk_fast.log)
+    const int fast = senv_int("STENCIL_TK_FAST", sched != nullptr ? 1 : 0);
     if (senv_int("STENCIL_TK_VERBOSE", 0)) {
         int per_cu = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0);
@@ -568,7 +604,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     }
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       avg_weight<T>(l.prob), sig, fsig, sched);
+                       avg_weight<T>(l.prob), sig, fsig, sched, fast);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }
@@ -621,6 +657,8 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 10608: return launch_st<double, 1, 6, 8, 4>(l, in, out, begin, end, s);
             case 404: return launch_st<double, 2, 4, 8, 4>(l, in, out, begin, end, s);
             case 510708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
+            // the default shape without the interior fast path (no duplicated step)
+            case 710708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, false>(l, in, out, begin, end, s);
             case 510608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
             case 610608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
             case 610508: return launch_st<double, 1, 5, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
