@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -88,6 +89,10 @@ struct Slab {
     hipStream_t sa = nullptr, sb = nullptr;    // boundary + exchange (high priority) / interior
     hipEvent_t ev_bnd = nullptr, ev_int = nullptr, ev_join = nullptr;
     ncclComm_t comm = nullptr;
+    // face-signalled rounds: [0] low-face adds, [1] high-face adds (they run
+    // on across launches), [2] the wait kernel's timeout flag
+    uint32_t* counters = nullptr;
+    uint32_t sig_target = 0;  // adds per face expected once the last queued launch is done
 };
 
 }  // namespace
@@ -101,6 +106,7 @@ struct stencil_slab_job {
     int depth = 1;   // halo planes exchanged per face
     bool cur_is_a = true;
     bool chained = false;  // round events recorded since the last join
+    bool signal = false;   // full rounds as face-signalled single launches
     std::vector<stencil::Slab> s;
 };
 
@@ -249,6 +255,54 @@ int slab_round(stencil_slab_job& j, int k) {
     return STENCIL_OK;
 }
 
+// One round of `k` fused sweeps as ONE face-signalled launch per slab
+// (stencil_sweepk_signal; the slab.py rounds): the launch's
+// first z-chunk marches up and its last down, so its face planes are among the
+// first stored; the workgroups storing them add to the slab's counters.  The
+// exchange stream queues a wait for the counts (stencil_wait_counters) and the
+// halo exchange behind it, so the faces leave while the rest of the launch
+// runs -- no separate boundary launches.  Order: launch(r) reads the halos
+// exchange(r-1) received (B waits for A); exchange(r) receives into the halo
+// planes launch(r-1) read, and starts only once launch(r) has signalled, i.e.
+// after launch(r-1) ended (one stream).
+int slab_round_signal(stencil_slab_job& j, int k) {
+    const bool src_a = j.cur_is_a;
+    for (Slab& s : j.s) {
+        if (int rc = set_dev(s.device)) return rc;
+        void* src = src_a ? s.a : s.b;
+        void* dst = src_a ? s.b : s.a;
+        if (j.chained) STENCIL_HIP_CHECK(hipStreamWaitEvent(s.sb, s.ev_bnd, 0));
+        int nsig = 0;
+        if (int rc = stencil_sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, nullptr, &nsig, s.sb)) return rc;
+        STENCIL_HIP_CHECK(hipEventRecord(s.ev_int, s.sb));
+        s.sig_target += uint32_t(nsig);
+        if (int rc = stencil_wait_counters(s.counters, s.sig_target, s.sig_target, s.counters + 2, s.sa)) return rc;
+    }
+    if (int rc = exchange(j, !src_a)) return rc;
+    for (Slab& s : j.s) {
+        if (int rc = set_dev(s.device)) return rc;
+        STENCIL_HIP_CHECK(hipEventRecord(s.ev_bnd, s.sa));
+        // the next round's boundary-launch path (remainders) writes planes
+        // this launch reads: A must also follow B
+        STENCIL_HIP_CHECK(hipStreamWaitEvent(s.sa, s.ev_int, 0));
+    }
+    j.chained = true;
+    j.cur_is_a = !src_a;
+    return STENCIL_OK;
+}
+
+// Did a face-counter wait give up (10 s)?  Then the halos are wrong.
+int check_signal_timeouts(stencil_slab_job& j) {
+    for (Slab& s : j.s) {
+        if (!s.counters) continue;
+        if (int rc = set_dev(s.device)) return rc;
+        uint32_t flag = 0;
+        STENCIL_HIP_CHECK(hipMemcpy(&flag, s.counters + 2, sizeof(flag), hipMemcpyDeviceToHost));
+        if (flag) return set_error(STENCIL_EHIP, "slab on device %d: a face-counter wait timed out", s.device);
+    }
+    return STENCIL_OK;
+}
+
 void release(stencil_slab_job* j) {
     if (!j) return;
     for (Slab& s : j->s) {
@@ -263,6 +317,7 @@ void release(stencil_slab_job* j) {
         if (s.ev_bnd) (void)hipEventDestroy(s.ev_bnd);
         if (s.ev_int) (void)hipEventDestroy(s.ev_int);
         if (s.ev_join) (void)hipEventDestroy(s.ev_join);
+        if (s.counters) (void)hipFree(s.counters);
     }
     delete j;
 }
@@ -302,6 +357,22 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
     j->periodic = flags & STENCIL_SLAB_PERIODIC;
     j->k = fuse_depth(g);
     j->depth = std::max<int>(j->k, g.radius);
+    // face-signalled rounds where the K-step kernels have them (3D r = 1 naive
+    // 7-point star K = 3..5, box K = 2..3); STENCIL_SLAB_SIGNAL=0: boundary +
+    // interior launches
+    {
+        const char* e = std::getenv("STENCIL_SLAB_SIGNAL");
+        const bool star = g.shape == STENCIL_STAR && j->k >= 3 && j->k <= 5;
+        const bool box = g.shape == STENCIL_BOX && j->k >= 2 && j->k <= 3;
+        // and only with one slab per GPU: slabs sharing a GPU multiplex their
+        // streams onto its few hardware queues, where a polling wait kernel
+        // could sit in front of the launch another slab's wait is polling for
+        bool distinct = true;
+        for (int i = 0; i < ngpus; ++i)
+            for (int k = 0; k < i; ++k) distinct = distinct && devs[size_t(i)] != devs[size_t(k)];
+        j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct &&
+                    !(e && *e == '0');
+    }
     const int64_t base = g.nz / ngpus, rem = g.nz % ngpus;
     j->s.resize(size_t(ngpus));
     int rc = STENCIL_OK;
@@ -330,6 +401,9 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
             hipEventCreateWithFlags(&s.ev_int, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming) != hipSuccess)
             rc = set_error(STENCIL_EHIP, "stream / event creation failed on device %d", s.device);
+        if (rc == STENCIL_OK && (hipMalloc(&s.counters, 4 * sizeof(uint32_t)) != hipSuccess ||
+                                 hipMemset(s.counters, 0, 4 * sizeof(uint32_t)) != hipSuccess))
+            rc = set_error(STENCIL_EHIP, "face counters on device %d", s.device);
     }
     if (rc == STENCIL_OK && exchange_kind == STENCIL_EXCHANGE_RCCL) {
         std::vector<ncclComm_t> comms(size_t(ngpus), nullptr);
@@ -405,10 +479,12 @@ int stencil_slab_run(stencil_slab_job* job, uint32_t iterations, float* elapsed_
     uint32_t done = 0;
     const uint32_t k = uint32_t(job->k);
     for (; done + k <= iterations; done += k)
-        if (int rc = slab_round(*job, int(k))) return rc;
+        if (int rc = job->signal ? slab_round_signal(*job, int(k)) : slab_round(*job, int(k))) return rc;
     if (done < iterations)  // the remainder as one shorter fused round
         if (int rc = slab_round(*job, int(iterations - done))) return rc;
     if (int rc = sync_all(*job)) return rc;
+    if (job->signal)
+        if (int rc = check_signal_timeouts(*job)) return rc;
     const auto t1 = std::chrono::steady_clock::now();
     if (elapsed_ms) *elapsed_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
     clear_error();

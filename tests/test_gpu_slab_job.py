@@ -68,6 +68,31 @@ def test_slab_job_matches_oracle_and_upload(gpu):
     job.close()
 
 
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("shape_name", ["star", "box"])
+@pytest.mark.parametrize("exchange", ["copy", "rccl"])
+def test_slab_job_signalled_rounds_equal_boundary_launches(gpu, monkeypatch, dtype, shape_name, exchange):
+    """One slab per GPU: full rounds are ONE face-signalled launch per slab
+    (the exchange waits on the face counters, csrc/slab.hip
+    slab_round_signal); STENCIL_SLAB_SIGNAL=0 gives boundary + interior
+    launches.  A periodic ring of one slab (its faces are its own halos, so
+    both faces cross the exchange every round), full rounds and a remainder,
+    bitwise equal both ways."""
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape_name)
+    shape = (131, 61, 47)
+    res = []
+    for sig in ("1", "0"):
+        monkeypatch.setenv("STENCIL_SLAB_SIGNAL", sig)
+        job = SlabJob(spec, *shape, devices=[gpu], exchange=exchange, periodic=True)
+        k = job.info(0)["sweeps_per_round"]
+        job.fill_initial("random", 23)
+        job.run(4 * k + 1)
+        job.run(k)
+        res.append(job.download())
+        job.close()
+    assert same_bits(res[0], res[1])
+
+
 @pytest.mark.parametrize("shape_name", ["star", "box"])
 def test_slab_job_rccl_self_ring_equals_copies(gpu, shape_name):
     """The RCCL exchange (ncclCommInitAll over one device, a periodic ring of
