@@ -97,6 +97,8 @@ def parse():
                     help="rehearsal: every rank uses GPU 0 (needs --exchange host)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N>1: skip the bitwise check against the global grid run as one grid on rank 0")
     return ap.parse_args()
 
 
@@ -144,6 +146,53 @@ def load_traffic(workload_key: str, kernel_name: str):
         return None, None
     fresh = ent.get("kernel_source_sha") == kernel_source_sha(kernel_name)
     return (ent.get("hbm_bytes_per_launch") if fresh else None), dict(ent, fresh=fresh)
+
+
+def verify_slabs(eng, slab, spec, grid, world, rank, sweeps, on_gpu, local):
+    """End-to-end check of a multi-GPU run, after the timed region: every
+    rank's per-plane sums (fp64, one deterministic sum per plane) gathered on
+    rank 0 and compared BIT FOR BIT with the same number of sweeps of the
+    whole global grid run as ONE grid on rank 0's GPU -- the slabs' exchange,
+    fused rounds and face signalling must not change a single bit (SURVEY
+    8(e)).  Skipped when the global grid does not fit beside rank 0's slab."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from stencil_amd.engine import JacobiEngine
+    from stencil_amd.slab import partition
+
+    gnx, gny, gnz = grid
+    counts = [partition(gnz, world, r)[1] for r in range(world)]
+    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    buf = torch.zeros(max(counts), dtype=torch.float64)
+    buf[:counts[rank]] = torch.from_numpy(eng.plane_sums(slab.cur))
+    buf = buf.to(dev)
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    result = None
+    if rank == 0:
+        try:
+            got = np.concatenate([parts[r].cpu().numpy()[:counts[r]] for r in range(world)])
+            need = 2.2 * gnx * gny * gnz * spec.elem_bytes  # two padded grids
+            free = torch.cuda.mem_get_info(local)[0]
+            if need > 0.9 * free:
+                result = {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free"}
+            else:
+                ref = JacobiEngine(dataclasses.replace(spec, halo=0), gnx, gny, gnz, device=local)
+                ref.reset("reference")
+                fin, _ = ref.iterate(sweeps)
+                want = ref.plane_sums(fin)
+                bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
+                result = {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad,
+                          "bitwise_equal": bad == 0,
+                          "reference": "the global grid as one grid on rank 0's GPU, same sweeps, per-plane sums"}
+                del ref, fin
+                torch.cuda.empty_cache()
+        except Exception as exc:  # a check, never the measurement
+            result = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    dist.barrier()
+    return result
 
 
 def main():
@@ -253,10 +302,15 @@ def main():
         # events are extra queue packets (~5 us each per round on MI355X) that
         # the timed rounds do not carry.
         slab.start_kernel_timing()
-        slab.run(max(4, min(args.steps, 8)) * slab.launches_per_round())
+        extra = max(4, min(args.steps, 8)) * slab.launches_per_round()
+        slab.run(extra)
         kernel_ms_total, kernel_launches = slab.stop_kernel_timing()
         if world > 1:
             dist.barrier()
+    check = None
+    if world > 1 and not args.no_check:
+        check = verify_slabs(eng, slab, spec, (gnx, gny, gnz), world, rank, args.warmup + args.steps + extra,
+                             args.exchange == "nccl", local)
 
     cells_per_gpu = float(gnx) * gny * count  # this rank's; rank 0 owns the largest slab
     total_updates = float(gnx) * gny * gnz * args.steps
@@ -340,6 +394,8 @@ def main():
                                   "events around the interior launches of extra rounds after the timed region"),
             },
         }
+        if world > 1:
+            out["multi_gpu_check"] = check if check is not None else {"skipped": "--no-check"}
         if traffic_entry is not None:
             out["roofline"]["traffic_source"] = {k: traffic_entry.get(k) for k in
                                                  ("source", "kernel", "kernel_source_sha", "fresh")}
