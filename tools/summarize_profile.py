@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def short(name):
     """Kernel family name as bench.py reports it."""
     table = (("tkstrip_7pt", "temporalk"), ("temporalk_7pt", "temporalk"), ("temporal2_7pt", "temporal2"),
-             ("zmarch7", "zmarch"), ("sweep_direct", "direct"), ("box27_sep", "boxk"), ("boxk_27pt", "boxk"),
+             ("zmarch7", "zmarch"), ("sweep_direct", "direct"), ("box27_sep", "boxk"), ("box27_strip", "boxk"), ("boxk_27pt", "boxk"),
              ("copy_kernel", "copy_kernel"), ("fill_initial_kernel", "fill_initial_kernel"),
              ("plane_sums", "plane_sums"))
     for k, v in table:
