@@ -49,7 +49,7 @@ PRESETS = {
     "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=2,
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
     "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
-               desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, temporal blocking (3 sweeps per launch, "
+               desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, temporal blocking (4 sweeps per launch, "
                     "deeper than the config's 2; bitwise the same result)"),
     # north_star's 4096^3 fp64 needs 2 x 550 GB; its largest single-GPU
     # proxy is 2048^3 fp64: 2 x 70 GB with ghosts and padding
@@ -241,7 +241,7 @@ def main():
         gnx, gny, gnz = pre["grid"]
         first, count = partition(gnz, world, rank)
     # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
-    # 4 for the 7-point star, 2 for the box) so K sweeps fuse across the
+    # 4 for the 7-point star, 3 or 4 for the box) so K sweeps fuse across the
     # exchange too (one K-plane exchange per K-sweep round).
     spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
     fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps

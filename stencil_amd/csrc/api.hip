@@ -142,16 +142,19 @@ int iterate_tk_steps(const stencil_problem& p) {
 }
 
 // Sweeps per launch of the 27-point box in stencil_iterate (AUTO, or explicit
-// TEMPORALK): K = 3 launches of kernels_boxk.hip, remainder as a pair / single
-// (STENCIL_BOX_STEPS=2: pairs only).  Measured (tools/box_k3_ab.sh,
-// profiles/r02e_ab_box_k3.log): 2048^2 x 256 fp64 717 vs 651 Gcell/s for pairs,
-// fp32 1242 vs 1182; 512^3 equal.  0 = not used.
+// TEMPORALK): K-step launches of kernels_boxk.hip, remainder as a pair / single
+// (STENCIL_BOX_STEPS=3|4 forces K, 2: pairs only).  K = 3 beat pairs
+// (profiles/r02e_ab_box_k3.log: 2048^2 x 256 fp64 717 vs 651 Gcell/s, fp32
+// 1242 vs 1182); K = 4 (strip 3 x 8) beats K = 3 for fp64 planes of >= 1024^2
+// cells (2048^2 x 256 808 vs 686, 2048^3 861 vs 652) but not at 512^3 (733 vs
+// 778) nor in fp32, where its shape spills (882 vs 1506;
+// profiles/r02u_ab_box_k4.log).  0 = not used.
 int iterate_box_steps(const stencil_problem& p) {
     if (!box27_supports(p)) return 0;
     if (!(p.kernel == STENCIL_KERNEL_TEMPORALK || (p.kernel == STENCIL_KERNEL_AUTO && iterate_fused(p)))) return 0;
     const char* k = std::getenv("STENCIL_BOX_STEPS");
-    const int steps = k && *k ? std::atoi(k) : 3;
-    return steps == 3 ? 3 : 0;
+    const int steps = k && *k ? std::atoi(k) : (p.dtype == STENCIL_F64 && p.nx * p.ny >= (int64_t(1) << 20) ? 4 : 3);
+    return steps == 3 || steps == 4 ? steps : 0;
 }
 
 // 2D problems iterate K sweeps per launch with the tile resident in LDS
@@ -478,9 +481,9 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
     if (int rc = check_layout(l)) return rc;
     if (steps < 3 || steps > 5) return set_error(STENCIL_EINVAL, "steps must be 1..5 (got %d)", steps);
     const bool box = box27_supports(l->prob);
-    if (!temporal2_supports(l->prob) && !(box && steps == 3))
+    if (!temporal2_supports(l->prob) && !(box && steps <= 4))
         return set_error(STENCIL_EUNSUPPORTED,
-                         "3- and 4-step fused sweeps cover the 3D r=1 naive 7-point star (3, 4) and box (3) only");
+                         "3- to 5-step fused sweeps cover the 3D r=1 naive 7-point star (3..5) and box (3, 4) only");
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");

@@ -1,5 +1,5 @@
 // kernels_boxk.hip -- the 3D 27-point box stencil (r = 1, naive order):
-// K = 1, 2 or 3 sweeps per launch, z-marching with SEPARABLE partial sums.
+// K = 1 .. 4 sweeps per launch, z-marching with SEPARABLE partial sums.
 //
 // Sum order (no reference code for the box; defined in DESIGN.md §3 and
 // restated by oracle/oracle_impl.inc):
@@ -572,10 +572,11 @@ __global__ void __launch_bounds__(64 * NW)
                 }
             }
         }
-        if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? K - 1 : 1)>{});
-        if constexpr (K >= 3) stage(std::integral_constant<int, 1>{});
-        if constexpr (K == 2) stage(std::integral_constant<int, 1>{});
-        static_assert(K >= 1 && K <= 3, "K = 1..3");
+        // stages K-1 .. 1
+        if constexpr (K >= 4) stage(std::integral_constant<int, (K >= 4 ? K - 1 : 1)>{});
+        if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? 2 : 1)>{});
+        if constexpr (K >= 2) stage(std::integral_constant<int, 1>{});
+        static_assert(K >= 1 && K <= 4, "K = 1..4");
         // stage 1's next input plane: in(p)
         *reinterpret_cast<VT*>(&L[PW][0][w][0][xl]) = rsum(vin[S][0]);
         *reinterpret_cast<VT*>(&L[PW][0][w][1][xl]) = rsum(vin[S][RY - 1]);
@@ -697,6 +698,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         if (l.prob.dtype == STENCIL_F32) {
             switch (steps * 1000000 + cfg) {
             case 3920408: return launch_bk<float, 2, 4, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 4920308: return launch_bk<float, 2, 3, 8, 4, false, true>(l, in, out, begin, end, s);
+            case 4920408: return launch_bk<float, 2, 4, 8, 4, false, true>(l, in, out, begin, end, s);
             case 3920312: return launch_bk<float, 2, 3, 12, 3, false, true>(l, in, out, begin, end, s);
             case 2920408: return launch_bk<float, 2, 4, 8, 2, false, true>(l, in, out, begin, end, s);
             case 2920312: return launch_bk<float, 2, 3, 12, 2, false, true>(l, in, out, begin, end, s);
@@ -708,6 +711,9 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         } else {
             switch (steps * 1000000 + cfg) {
             case 3910408: return launch_bk<double, 1, 4, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 4910308: return launch_bk<double, 1, 3, 8, 4, false, true>(l, in, out, begin, end, s);
+            case 4910408: return launch_bk<double, 1, 4, 8, 4, false, true>(l, in, out, begin, end, s);
+            case 4910216: return launch_bk<double, 1, 2, 16, 4, false, true>(l, in, out, begin, end, s);
             case 3910312: return launch_bk<double, 1, 3, 12, 3, false, true>(l, in, out, begin, end, s);
             case 3910212: return launch_bk<double, 1, 2, 12, 3, false, true>(l, in, out, begin, end, s);
             case 3910308: return launch_bk<double, 1, 3, 8, 3, false, true>(l, in, out, begin, end, s);
@@ -782,7 +788,11 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         default: break;
         }
     }
-    return set_error(STENCIL_EINVAL, "box kernel steps must be 1, 2 or 3 (got %d)", steps);
+    if (steps == 4) {  // strip layout, 3 rows x 8 waves (4 rows spill)
+        if (l.prob.dtype == STENCIL_F32) return launch_bk<float, 2, 3, 8, 4, false, true>(l, in, out, begin, end, s);
+        return launch_bk<double, 1, 3, 8, 4, false, true>(l, in, out, begin, end, s);
+    }
+    return set_error(STENCIL_EINVAL, "box kernel steps must be 1..4 (got %d)", steps);
 }
 
 // Face-signalled box launches for multi-GPU slab rounds (stencil_sweepk_signal):
@@ -804,6 +814,9 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
             case 3910408: return launch_bk<double, 1, 4, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             case 3910308: return launch_bk<double, 1, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             case 3910312: return launch_bk<double, 1, 3, 12, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4910308: return launch_bk<double, 1, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4910212: return launch_bk<double, 1, 2, 12, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4910216: return launch_bk<double, 1, 2, 16, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             default: break;
             }
         }
@@ -832,7 +845,12 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
         default: break;
         }
     }
-    return set_error(STENCIL_EINVAL, "face-signalled box sweeps: steps must be 2 or 3 (got %d)", steps);
+    if (steps == 4) {  // strip layout, 3 rows x 8 waves (as launch_boxk)
+        if (l.prob.dtype == STENCIL_F32)
+            return launch_bk<float, 2, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        return launch_bk<double, 1, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+    }
+    return set_error(STENCIL_EINVAL, "face-signalled box sweeps: steps must be 2..4 (got %d)", steps);
 }
 
 // Single sweeps and fused pairs of the box (stencil_sweep / stencil_sweep2).

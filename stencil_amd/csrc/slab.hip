@@ -358,12 +358,12 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
     j->k = fuse_depth(g);
     j->depth = std::max<int>(j->k, g.radius);
     // face-signalled rounds where the K-step kernels have them (3D r = 1 naive
-    // 7-point star K = 3..5, box K = 2..3); STENCIL_SLAB_SIGNAL=0: boundary +
+    // 7-point star K = 3..5, box K = 2..4); STENCIL_SLAB_SIGNAL=0: boundary +
     // interior launches
     {
         const char* e = std::getenv("STENCIL_SLAB_SIGNAL");
         const bool star = g.shape == STENCIL_STAR && j->k >= 3 && j->k <= 5;
-        const bool box = g.shape == STENCIL_BOX && j->k >= 2 && j->k <= 3;
+        const bool box = g.shape == STENCIL_BOX && j->k >= 2 && j->k <= 4;
         // and only with one slab per GPU: slabs sharing a GPU multiplex their
         // streams onto its few hardware queues, where a polling wait kernel
         // could sit in front of the launch another slab's wait is polling for

@@ -128,11 +128,11 @@ class JacobiEngine:
     @property
     def supports_signal(self) -> bool:
         """Face-signalled K-step launches (stencil_sweepk_signal): the 3D 7-point
-        star (K = 3..5) and the 27-point box (K = 2, 3)."""
+        star (K = 3..5) and the 27-point box (K = 2..4)."""
         s = self.spec
         if not (s.dims == 3 and s.radius == 1 and s.order == "naive" and self.fused):
             return False
-        return 3 <= self.fuse_steps <= 5 if s.shape == "star" else 2 <= self.fuse_steps <= 3
+        return 3 <= self.fuse_steps <= 5 if s.shape == "star" else 2 <= self.fuse_steps <= 4
 
     def sweepk_signal(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int,
                       counters: torch.Tensor, stream=None, face_signal: "FaceSignal | None" = None) -> int:

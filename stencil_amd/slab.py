@@ -27,7 +27,7 @@ A round is one sweep (halo depth r), or -- when the backend has a fused
 multi-step kernel and K-deep halos -- K sweeps in one launch per plane range
 (temporal blocking across GPUs: the exchange of K planes every K sweeps, the
 halo planes themselves advanced to t+K-1 .. t+1 on chip by the fused kernel;
-K = 4 for the 7-point star, 2 for the 27-point box).
+K = the library's fuse depth: 4 for the 7-point star, 3 or 4 for the 27-point box).
 Every cell's arithmetic is the single-GPU kernel's, so results are bitwise
 identical for any number of ranks (tests/test_slab_gloo.py, tests/test_gpu_*).
 

@@ -379,13 +379,14 @@ def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
     assert e.plan(8) == (3, 3)
 
 
-BOX_STRIP_CFGS = {"fp64": {3: ["910408", "910308", "910312", "910212", "910216"], 2: ["910408", "910312", "910216"],
-                            1: ["920408"]},
-                   "fp32": {3: ["920408", "920312", "920216"], 2: ["920408", "920312", "940208"], 1: ["940408"]}}
+BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910216"], 3: ["910408", "910308", "910312", "910212", "910216"],
+                            2: ["910408", "910312", "910216"], 1: ["920408"]},
+                   "fp32": {4: ["920308", "920408"], 3: ["920408", "920312", "920216"], 2: ["920408", "920312", "940208"],
+                            1: ["940408"]}}
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("steps", [1, 2, 3])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (7, 5, 3), (250, 119, 12), (64, 300, 40)])
 @pytest.mark.parametrize("zchunk", ["0", "5", "13"])
 def test_box_strip_shapes(gpu, monkeypatch, dtype, steps, shape3, zchunk):
@@ -552,7 +553,8 @@ def test_full_size_baseline_configs(gpu, cfg):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("case", ["C2_512cube_fp64", "C3_4096sq_x32_fp32", "C4_2048sq_x512_fp64"])
+@pytest.mark.parametrize("case", ["C2_512cube_fp64", "C3_4096sq_x32_fp32", "C4_2048sq_x512_fp64",
+                                  "C5_2048sq_x256_box_fp64", "box_512cube_fp64", "box_2048sq_x64_fp32"])
 def test_benched_kernel_at_benched_shape(gpu, case):
     """The kernels that produce the bench numbers, at the shapes they are
     benched on, through AUTO, bitwise against the multithreaded oracle --
@@ -562,24 +564,32 @@ def test_benched_kernel_at_benched_shape(gpu, case):
       C3: 4096^2 x 32 fp32, 10 sweeps = two K = 5 launches (AUTO's K for fp32
           planes >= 1024^2);
       C4: 2048^2 x 512 fp64 (one GPU's slab of config 4), 8 sweeps = two
-          K = 4 launches of equal z-chunks (too many tiles to pack)."""
+          K = 4 launches of equal z-chunks (too many tiles to pack);
+      C5: 2048^2 x 256 fp64 box (one GPU's slab of config 5), 9 sweeps = two
+          K = 4 strip launches (fp64 planes >= 1024^2) + a single sweep;
+      box 512^3 fp64 (K = 3 strip 4 x 8) and 2048^2 x 64 fp32 (K = 3 strip)."""
     import torch
     from stencil_amd import _lib
-    shapes = {"C2_512cube_fp64": ("fp64", (512, 512, 512), 9, 4, (3, _lib.KERNEL_TEMPORALK), True),
-              "C3_4096sq_x32_fp32": ("fp32", (4096, 4096, 32), 10, 5, (2, _lib.KERNEL_TEMPORALK), False),
-              "C4_2048sq_x512_fp64": ("fp64", (2048, 2048, 512), 8, 4, (2, _lib.KERNEL_TEMPORALK), False)}
-    dtype, (nx, ny, nz), it, k, plan, packed = shapes[case]
-    e = engine(gpu, 3, dtype, "star", 1, "naive", "auto", nx, ny, nz)
+    t2 = _lib.KERNEL_TEMPORAL2  # the box's fused family reports TEMPORAL2
+    shapes = {"C2_512cube_fp64": ("star", "fp64", (512, 512, 512), 9, 4, (3, _lib.KERNEL_TEMPORALK), True),
+              "C3_4096sq_x32_fp32": ("star", "fp32", (4096, 4096, 32), 10, 5, (2, _lib.KERNEL_TEMPORALK), False),
+              "C4_2048sq_x512_fp64": ("star", "fp64", (2048, 2048, 512), 8, 4, (2, _lib.KERNEL_TEMPORALK), False),
+              "C5_2048sq_x256_box_fp64": ("box", "fp64", (2048, 2048, 256), 9, 4, (3, t2), None),
+              "box_512cube_fp64": ("box", "fp64", (512, 512, 512), 7, 3, (3, t2), None),
+              "box_2048sq_x64_fp32": ("box", "fp32", (2048, 2048, 64), 6, 3, (2, t2), None)}
+    shape, dtype, (nx, ny, nz), it, k, plan, packed = shapes[case]
+    e = engine(gpu, 3, dtype, shape, 1, "naive", "auto", nx, ny, nz)
     assert e.fuse_steps == k
     assert e.plan(it) == plan
-    geo = e.sweepk_geometry(k)
-    assert geo["packed"] == packed, geo
+    if packed is not None:
+        geo = e.sweepk_geometry(k)
+        assert geo["packed"] == packed, geo
     e.reset("random", 4242)
     fin, _ = e.iterate(it)
     got = e.interior(fin).cpu().numpy()
     del e, fin
     torch.cuda.empty_cache()
-    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
+    p = ob.problem(3, dtype, shape, 1, "naive", nx, ny, nz)
     want = ob.interior(p, ob.run(p, it, "random", 4242, threads=16))
     assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
 

@@ -198,10 +198,11 @@ def test_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, fla
 
 
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-@pytest.mark.parametrize("steps", [2, 3])
+@pytest.mark.parametrize("steps", [2, 3, 4])
 @pytest.mark.parametrize("zchunk", ["0", "5", "9", "40"])
 @pytest.mark.parametrize("flags", [0, 3])
-@pytest.mark.parametrize("cfg", ["0", "10308", "20308", "10208", "10116", "20116", "910408", "910312", "920408"])
+@pytest.mark.parametrize("cfg", ["0", "10308", "20308", "10208", "10116", "20116", "910408", "910312", "920408",
+                                 "910212", "910216"])
 def test_box_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, flags, cfg):
     """The 27-point box's face-signalled launch (kernels_boxk.hip SIG: the last
     z-chunk marches down, carrying C and two plane sums instead of the
@@ -209,7 +210,7 @@ def test_box_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk,
     monkeypatch.setenv("STENCIL_BOXK_ZCHUNK", zchunk)
     monkeypatch.setenv("STENCIL_BOXK_SIG_CFG", cfg)
     nx, ny, nz = 77, 51, 31
-    spec = StencilSpec(dims=3, dtype=dtype, shape="box", halo=3)
+    spec = StencilSpec(dims=3, dtype=dtype, shape="box", halo=4)
     e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=flags)
     e.reset("random", 9)
     ref = torch.empty_like(e.b)
