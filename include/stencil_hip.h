@@ -184,7 +184,7 @@ int stencil_sweep2(const stencil_layout* l, const void* in, void* out, int64_t b
                    void* stream);
 
 /* K fused sweeps, out = S^K(in) on [begin, end): steps 1 = stencil_sweep,
- * 2 = stencil_sweep2, 3..5 = the TEMPORALK kernel (3D 7-point star), 3 =
+ * 2 = stencil_sweep2, 3..5 = the TEMPORALK kernel (3D 7-point star), 3..4 =
  * the K-step box kernel (3D 27-point box; kernels_boxk.hip, which also serves
  * the box's 2-step sweep2).
  * With HALO_LO/HI flags the grid needs halo >= steps. */
@@ -200,7 +200,7 @@ int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end,
                             int32_t* zchunk, int32_t* packed);
 
 /* Multi-GPU slabs: stencil_sweepk over [begin, end) (3D 7-point star, steps
- * 3..5) as ONE launch whose workgroups add 1 to counters[0] as soon as the
+ * 3..5; 27-point box, steps 2..4) as ONE launch whose workgroups add 1 to counters[0] as soon as the
  * low face planes [begin, begin+steps) are stored and to counters[1] for
  * [end-steps, end) (the last z-chunk marches downward, so both faces come
  * first); *signals_per_face = adds per face per launch.  counters: two
