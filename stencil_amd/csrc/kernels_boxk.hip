@@ -38,12 +38,6 @@
 
 #include "common.hpp"
 
-#ifndef BOXS_OPAQUE
-#define BOXS_OPAQUE 0
-#endif
-#ifndef BOXS_SB
-#define BOXS_SB 0
-#endif
 
 namespace stencil {
 namespace {
@@ -314,9 +308,6 @@ __global__ void __launch_bounds__(64 * NW)
             }
         }
         load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
-#if BOXS_SB >= 1
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     };
 
     const int plast = zb - 1 + 2 * K;
@@ -413,16 +404,14 @@ __global__ void __launch_bounds__(64 * NW)
     }
     // R = (l + c) + r and E = l + r of a row vector (x-neighbours by DPP)
     auto sums = [&](const VT& v, VT& R, VT& E) {
-#if BOXS_SB >= 4
-        __builtin_amdgcn_sched_barrier(0);
-#endif
         const T wl = bdpp<kShr1>(v[V - 1]);
         const T er = bdpp<kShl1>(v[0]);
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
             const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
-            E[j] = l + r;
+            const T e = l + r;
+            E[j] = e;
             R[j] = (l + v[j]) + r;
         }
     };
@@ -445,9 +434,6 @@ __global__ void __launch_bounds__(64 * NW)
         const int z = zr(m);
         const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
-#if BOXS_OPAQUE
-        asm volatile("" : "+s"(base));  // keep base + 32-bit offset (saddr form)
-#endif
 #pragma unroll
         for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + row_off(off[k]));
     };
@@ -478,9 +464,6 @@ __global__ void __launch_bounds__(64 * NW)
         const int zo = p - 2 * K;  // t_K(zo) -> HBM this step
         const bool do_store = zo >= za && zo < zb;
         char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
-#if BOXS_OPAQUE
-        asm volatile("" : "+s"(obase));
-#endif
         auto stage = [&](auto s_) {
             constexpr int s = decltype(s_)::value;
             const int m = zr(p - 2 * s);  // plane of t_s finished now
@@ -538,13 +521,7 @@ __global__ void __launch_bounds__(64 * NW)
                 Rm = Rc;
                 Rc = Rn;
                 Ec = En;
-#if BOXS_SB >= 3
-                __builtin_amdgcn_sched_barrier(0);
-#endif
             }
-#if BOXS_SB >= 2
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         };
         stage(std::integral_constant<int, K>{});
         if constexpr (SIG) {
@@ -581,9 +558,6 @@ __global__ void __launch_bounds__(64 * NW)
         *reinterpret_cast<VT*>(&L[PW][0][w][0][xl]) = rsum(vin[S][0]);
         *reinterpret_cast<VT*>(&L[PW][0][w][1][xl]) = rsum(vin[S][RY - 1]);
         load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
-#if BOXS_SB >= 1
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     };
 
     const int plast = zb - 1 + 2 * K;

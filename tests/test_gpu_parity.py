@@ -379,10 +379,11 @@ def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
     assert e.plan(8) == (3, 3)
 
 
-BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910216"], 3: ["910408", "910308", "910312", "910212", "910216"],
+BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910216"],
+                            3: ["910408", "910308", "910312", "910212", "910216"],
                             2: ["910408", "910312", "910216"], 1: ["920408"]},
-                   "fp32": {4: ["920308", "920408"], 3: ["920408", "920312", "920216"], 2: ["920408", "920312", "940208"],
-                            1: ["940408"]}}
+                   "fp32": {4: ["920308", "920408"], 3: ["920408", "920312", "920216"],
+                            2: ["920408", "920312", "940208"], 1: ["940408"]}}
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
