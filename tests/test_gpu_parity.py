@@ -700,7 +700,10 @@ def test_cli_multi_gpu_slabs(gpu):
     runs = [base + ["-m", "HIPMultiGPU", "--dtype", "fp64"],
             base + ["-m", "HIPMultiGPU", "HIP", "--gpus", "3", "--share-device", "--exchange", "copy"],
             base + ["-m", "HIP", "--gpus", "4", "--share-device", "--exchange", "copy", "--points", "27",
-                    "--dtype", "fp64"]]
+                    "--dtype", "fp64"],
+            # 700^2 fp64 box planes: K = 4 launches, and over RCCL the face-signalled K = 4 rounds
+            [cli, "-s", "700", "-b", "1", "-i", "13", "--dims", "3", "--nz", "12", "--init", "random", "-c",
+             "-m", "HIPMultiGPU", "HIP", "--points", "27", "--dtype", "fp64"]]
     for args in runs:
         out = subprocess.run(args, capture_output=True, text=True, timeout=300)
         assert out.returncode == 0, out.stderr + out.stdout
