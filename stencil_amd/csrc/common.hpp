@@ -80,6 +80,15 @@ struct LaunchInfo {
 };
 extern thread_local LaunchInfo* tl_dry_launch;
 
+// The packed longest-first z-chunk schedule (kernels_strip.hip): for a grid of
+// few tiles, chunks of Lc planes per tile (the last one shorter) dispatched
+// longest first, Lc chosen by simulating the dispatcher with `fill` steps of
+// pipeline fill per chunk; a device table of {tile, first plane, planes} per
+// workgroup when it beats equal chunks of zc planes, else *sched untouched.
+// `family` keeps the caches of different kernels apart.
+int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
+                    const int** sched, int64_t* nb);
+
 // ---- kernel entry points (defined in kernels_*.hip) ----------------------
 int launch_direct(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
                   hipStream_t s);

@@ -92,7 +92,7 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_sep(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
               int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-              unsigned long long* __restrict__ fsig) {
+              unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LY = Tl::LY, RW = Tl::RW;
@@ -351,7 +351,7 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_strip(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
                 int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW;
@@ -360,17 +360,29 @@ __global__ void __launch_bounds__(64 * NW)
     // boundary row sums: [step parity][stage input][wave][first, last row][RW]
     __shared__ __attribute__((aligned(16))) T L[2][K][NW][2][RW];
 
-    const int t = blockIdx.x;
+    // work: tile (bx, by) and planes [za, zb) -- equal z-chunks, or one entry
+    // {tile, first plane, planes} of the packed schedule (few-tile grids;
+    // never on the face-signalled launches)
+    int t = blockIdx.x, za, zb;
+    int64_t nch = 1;
+    if (!SIG && sched) {
+        const int* e = sched + 3 * int64_t(blockIdx.x);
+        t = e[0];
+        za = zbeg + e[1];
+        zb = za + e[2];
+    } else {
+        const int bz = t / (tiles_x * tiles_y);
+        za = zbeg + bz * zchunk;
+        zb = za + zchunk < zend ? za + zchunk : zend;
+        nch = (zend - zbeg + zchunk - 1) / zchunk;
+        t -= bz * tiles_x * tiles_y;
+    }
     const int bx = t % tiles_x;
-    const int by = (t / tiles_x) % tiles_y;
-    const int bz = t / (tiles_x * tiles_y);
+    const int by = t / tiles_x;
     const int lane = threadIdx.x, w = threadIdx.y;
     const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
     const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
-    const int za = zbeg + bz * zchunk;
-    const int zb = za + zchunk < zend ? za + zchunk : zend;
-    const int nch = (zend - zbeg + zchunk - 1) / zchunk;
-    const bool rev = SIG && nch >= 2 && bz == nch - 1;  // this workgroup's chunk marches down
+    const bool rev = SIG && nch >= 2 && zb == zend;  // this workgroup's chunk (the last) marches down
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
     const int64_t bias = g.row + XR * V;
@@ -613,10 +625,10 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         else return box27_sep<T, V, RY, NW, K, SIG>;
     }();
     int zc = env_int("STENCIL_BOXK_ZCHUNK", 0);
+    int slots = 0;
     if (zc <= 0) {
         // chunk count c minimising rounds x (chunk + 3K): a chunk's march
         // costs its planes plus the 3K-plane pipeline fill (kernels_strip.hip)
-        int slots = 0;
         if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
         int64_t best_c = 1, best = INT64_MAX;
         for (int64_t c = 1; c <= nz; ++c) {
@@ -646,11 +658,22 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (nsig) *nsig = int(tiles);
     }
     const int64_t gz = (nz + zc - 1) / zc;
-    const int64_t nb = tiles * gz;
+    int64_t nb = tiles * gz;
+    // few-tile grids: the packed longest-first schedule of the 7-point kernel
+    // with the box's 3K-plane pipeline fill; not on slabs.  fp64 only by
+    // default: 400^3 811 vs 755 Gcell/s, 512^3 796 vs 790, 640^2 x 320 equal;
+    // in fp32 it loses (512^3 1012 vs 1389, 640^2 x 320 1262 vs 1400) although
+    // the dispatcher model predicts 2-3 % fewer steps (profiles/r02dd_ab_box_pack.log)
+    const int* sched = nullptr;
+    if (STRIP && !SIG && slots > 0 && env_int("STENCIL_BOXK_PACK", sizeof(T) == 8 ? 1 : 0) && !(lo || hi)) {
+        int dev = 0;
+        STENCIL_HIP_CHECK(hipGetDevice(&dev));
+        if (const int rc = packed_schedule(1, dev, tiles, nz, K, 3 * K, slots, zc, &sched, &nb)) return rc;
+    }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
     hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
                        static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig);
+                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig, sched);
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
 }

@@ -413,93 +413,6 @@ int senv_int(const char* name, int dflt) {
     return s && *s ? std::atoi(s) : dflt;
 }
 
-// Makespan (in plane steps) of workgroups of the given plane counts on
-// `slots` one-workgroup CU slots: workgroup i goes to XCD i % 8 (the
-// dispatcher's round robin), and inside an XCD to the slot that frees first
-// (in-order dispatch); a chunk of n planes costs n + 2K steps (pipeline fill).
-int64_t simulate_makespan(const std::vector<int>& len, int K, int slots) {
-    constexpr int kXcd = 8;
-    const int per = std::max(1, slots / kXcd);
-    std::vector<std::vector<int64_t>> free_at(kXcd, std::vector<int64_t>(per, 0));
-    int64_t span = 0;
-    for (size_t i = 0; i < len.size(); ++i) {
-        auto& f = free_at[i % kXcd];
-        auto it = std::min_element(f.begin(), f.end());
-        *it += len[i] + 2 * K;
-        span = std::max(span, *it);
-    }
-    return span;
-}
-
-// STENCIL_TK_PACK (default 1; 0 = equal chunks): chunks of Lc planes per tile (the last one
-// shorter), longest first -- every tile's full chunks start in z lock-step,
-// the short remainders fill the CUs the full chunks leave idle.  Lc is the
-// one with the shortest simulated makespan; used only when it beats the
-// equal-chunk grid (zc planes per chunk) by 2 %.  The table is built once per
-// shape and kept for the process.
-// The table lives in the memory of the device it was built on: the cache is
-// keyed by device ordinal and guarded (a process may drive several GPUs from
-// several threads: stencil_set_device is per thread).
-int packed_schedule(int dev, int64_t tiles, int64_t nz, int K, int slots, int zc, const int** sched, int64_t* nb) {
-    // Only grids of few tiles: with more than 2 tiles per slot the equal
-    // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
-    // Gcell/s), and the search would cost host time at the first launch.
-    if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
-    if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
-    static std::mutex mu;
-    static std::map<std::tuple<int, int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    const auto key = std::make_tuple(dev, tiles, nz, K, slots);
-    auto hit = cache.find(key);
-    if (hit == cache.end()) {
-        auto build = [&](int64_t lc, std::vector<int>& tab) {
-            lc = std::max<int64_t>(1, lc);
-            struct Item { int len, c, t, z; };
-            std::vector<Item> items;
-            for (int64_t t = 0; t < tiles; ++t)
-                for (int64_t z = 0, c = 0; z < nz; z += lc, ++c)
-                    items.push_back({int(std::min<int64_t>(lc, nz - z)), int(c), int(t), int(z)});
-            std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
-                return a.len != b.len ? a.len > b.len : (a.c != b.c ? a.c < b.c : a.t < b.t);
-            });
-            std::vector<int> len;
-            tab.clear();
-            for (const Item& it : items) {
-                len.push_back(it.len);
-                tab.insert(tab.end(), {it.t, it.z, it.len});
-            }
-            return simulate_makespan(len, K, slots);
-        };
-        std::vector<int> tab, best_tab;
-        const int64_t base = build(zc, tab);
-        int64_t best = base;
-        for (int64_t lc = std::max<int64_t>(2 * K, nz / 16); lc <= nz; lc += std::max<int64_t>(1, nz / 256)) {
-            const int64_t m = build(lc, tab);
-            if (m < best) best = m, best_tab = tab;
-        }
-        int* d = nullptr;
-        int64_t n = 0;
-        if (!best_tab.empty() && best * 50 < base * 49) {
-            if (hipMalloc(&d, best_tab.size() * sizeof(int)) != hipSuccess ||
-                hipMemcpy(d, best_tab.data(), best_tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-                // a pageable H2D copy may return before its DMA lands, and the
-                // launch goes to another stream: wait for it (once per shape)
-                hipDeviceSynchronize() != hipSuccess)
-                return set_error(STENCIL_EHIP, "packed schedule upload failed");
-            n = int64_t(best_tab.size() / 3);
-        }
-        if (senv_int("STENCIL_TK_VERBOSE", 0))
-            std::fprintf(stderr, "tkstrip pack: equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n",
-                         (long long)base, (long long)best, (long long)n, d ? "" : " -- not used");
-        hit = cache.emplace(key, std::make_pair(d, n)).first;
-    }
-    if (hit->second.first) {
-        *sched = hit->second.first;
-        *nb = hit->second.second;
-    }
-    return STENCIL_OK;
-}
-
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
           bool FP = true>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
@@ -576,7 +489,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     // multi-GPU job, whose one-round grid above is deliberate
     if (!SIG && zc > 0 && senv_int("STENCIL_TK_PACK", 1) && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
         !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
-        const int rc = packed_schedule(dev, gx * gy, nz, K, slots, zc, &sched, &nb);
+        const int rc = packed_schedule(0, dev, gx * gy, nz, K, 2 * K, slots, zc, &sched, &nb);
         if (rc != STENCIL_OK) return rc;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
@@ -610,6 +523,96 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
 }
 
 }  // namespace
+
+// Makespan (in plane steps) of workgroups of the given plane counts on
+// `slots` one-workgroup CU slots: workgroup i goes to XCD i % 8 (the
+// dispatcher's round robin), and inside an XCD to the slot that frees first
+// (in-order dispatch); a chunk of n planes costs n + fill steps (pipeline fill:
+// 2K for the 7-point strip kernel, 3K for the box's).
+static int64_t simulate_makespan(const std::vector<int>& len, int fill, int slots) {
+    constexpr int kXcd = 8;
+    const int per = std::max(1, slots / kXcd);
+    std::vector<std::vector<int64_t>> free_at(kXcd, std::vector<int64_t>(per, 0));
+    int64_t span = 0;
+    for (size_t i = 0; i < len.size(); ++i) {
+        auto& f = free_at[i % kXcd];
+        auto it = std::min_element(f.begin(), f.end());
+        *it += len[i] + fill;
+        span = std::max(span, *it);
+    }
+    return span;
+}
+
+// STENCIL_TK_PACK (default 1; 0 = equal chunks): chunks of Lc planes per tile (the last one
+// shorter), longest first -- every tile's full chunks start in z lock-step,
+// the short remainders fill the CUs the full chunks leave idle.  Lc is the
+// one with the shortest simulated makespan; used only when it beats the
+// equal-chunk grid (zc planes per chunk) by 2 %.  The table is built once per
+// shape and kept for the process.
+// The table lives in the memory of the device it was built on: the cache is
+// keyed by device ordinal and guarded (a process may drive several GPUs from
+// several threads: stencil_set_device is per thread).
+int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
+                    const int** sched, int64_t* nb) {
+    // Only grids of few tiles: with more than 2 tiles per slot the equal
+    // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
+    // Gcell/s), and the search would cost host time at the first launch.
+    if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
+    if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_tuple(family, dev, tiles, nz, K, slots);
+    auto hit = cache.find(key);
+    if (hit == cache.end()) {
+        auto build = [&](int64_t lc, std::vector<int>& tab) {
+            lc = std::max<int64_t>(1, lc);
+            struct Item { int len, c, t, z; };
+            std::vector<Item> items;
+            for (int64_t t = 0; t < tiles; ++t)
+                for (int64_t z = 0, c = 0; z < nz; z += lc, ++c)
+                    items.push_back({int(std::min<int64_t>(lc, nz - z)), int(c), int(t), int(z)});
+            std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+                return a.len != b.len ? a.len > b.len : (a.c != b.c ? a.c < b.c : a.t < b.t);
+            });
+            std::vector<int> len;
+            tab.clear();
+            for (const Item& it : items) {
+                len.push_back(it.len);
+                tab.insert(tab.end(), {it.t, it.z, it.len});
+            }
+            return simulate_makespan(len, fill, slots);
+        };
+        std::vector<int> tab, best_tab;
+        const int64_t base = build(zc, tab);
+        int64_t best = base;
+        for (int64_t lc = std::max<int64_t>(fill, nz / 16); lc <= nz; lc += std::max<int64_t>(1, nz / 256)) {
+            const int64_t m = build(lc, tab);
+            if (m < best) best = m, best_tab = tab;
+        }
+        int* d = nullptr;
+        int64_t n = 0;
+        if (!best_tab.empty() && best * 50 < base * 49) {
+            if (hipMalloc(&d, best_tab.size() * sizeof(int)) != hipSuccess ||
+                hipMemcpy(d, best_tab.data(), best_tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+                // a pageable H2D copy may return before its DMA lands, and the
+                // launch goes to another stream: wait for it (once per shape)
+                hipDeviceSynchronize() != hipSuccess)
+                return set_error(STENCIL_EHIP, "packed schedule upload failed");
+            n = int64_t(best_tab.size() / 3);
+        }
+        if (senv_int("STENCIL_TK_VERBOSE", 0))
+            std::fprintf(stderr, "pack (family %d): equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n", family,
+                         (long long)base, (long long)best, (long long)n, d ? "" : " -- not used");
+        hit = cache.emplace(key, std::make_pair(d, n)).first;
+    }
+    if (hit->second.first) {
+        *sched = hit->second.first;
+        *nb = hit->second.second;
+    }
+    return STENCIL_OK;
+}
+
 
 // cfg = RY*100 + NW (rows per wave x waves); 0 = default shape.
 int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,

@@ -554,6 +554,20 @@ def test_full_size_baseline_configs(gpu, cfg):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("pack", ["1", "0"])
+def test_box_packed_schedule(gpu, monkeypatch, pack):
+    """The box's packed longest-first z-chunk schedule (few-tile fp64 grids,
+    kernels_boxk.hip + kernels_strip.hip packed_schedule) at a shape where it
+    is used, 7 sweeps (two K = 3 launches + a single), bitwise against the
+    oracle -- and with it switched off."""
+    monkeypatch.setenv("STENCIL_BOXK_PACK", pack)
+    nx, ny, nz = 400, 400, 400  # 112 tiles: 336 packed workgroups (STENCIL_TK_VERBOSE=1 prints the table size)
+    p = ob.problem(3, "fp64", "box", 1, "naive", nx, ny, nz)
+    want = ob.run(p, 7, "random", 77, threads=16)
+    _, got = gpu_run(gpu, 3, "fp64", "box", 1, "naive", "auto", nx, ny, nz, 7, "random", 77)
+    assert same_bits(got, want)
+
+
 @pytest.mark.parametrize("case", ["C2_512cube_fp64", "C3_4096sq_x32_fp32", "C4_2048sq_x512_fp64",
                                   "C5_2048sq_x256_box_fp64", "box_512cube_fp64", "box_2048sq_x64_fp32"])
 def test_benched_kernel_at_benched_shape(gpu, case):
