@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
+#include <functional>
 
 #include "stencil_hip.h"
 
@@ -85,9 +87,26 @@ extern thread_local LaunchInfo* tl_dry_launch;
 // longest first, Lc chosen by simulating the dispatcher with `fill` steps of
 // pipeline fill per chunk; a device table of {tile, first plane, planes} per
 // workgroup when it beats equal chunks of zc planes, else *sched untouched.
-// `family` keeps the caches of different kernels apart.
+// `family` keeps the caches of different kernels apart.  *verdict (when
+// asked for) points at the shape's measured choice: kPackUntested until
+// pick_schedule has timed both grids on this device, then kPackPacked or
+// kPackEqual.
+enum { kPackUntested = 0, kPackPacked = 1, kPackEqual = 2 };
 int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    const int** sched, int64_t* nb);
+                    const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr);
+
+// The dispatcher model behind packed_schedule mispredicts some shapes badly
+// (measured: 504 x 512 x 512 fp64 packed 0.555 vs equal 0.450 ms per launch,
+// 256^3 -17 %, 448^3 -7 %, while 512^3 gains 8 %; profiles/r02gg_pack.log),
+// so the first launch of a shape times both grids on the caller's stream and
+// keeps the faster one.  launch(packed) enqueues ONE launch of the same
+// sweep (same in, same out: every trial writes identical bits).  Runs
+// 3 x (packed, equal) launches, blocks the host once for the events, records
+// the verdict.  On a capturing stream nothing is timed: the model's choice
+// is launched once (*launched = true either way unless an error is returned).
+int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<hipError_t(bool)>& launch);
+// STENCIL_TK_PACK / STENCIL_BOXK_PACK: 0 = equal chunks, 1 = measured choice
+// (default), 2 = the model's choice without measuring
 
 // ---- kernel entry points (defined in kernels_*.hip) ----------------------
 int launch_direct(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

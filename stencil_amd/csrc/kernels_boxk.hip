@@ -664,17 +664,29 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     // default: 400^3 811 vs 755 Gcell/s, 512^3 796 vs 790, 640^2 x 320 equal;
     // in fp32 it loses (512^3 1012 vs 1389, 640^2 x 320 1262 vs 1400) although
     // the dispatcher model predicts 2-3 % fewer steps (profiles/r02dd_ab_box_pack.log)
+    // (measured choice on the first launch of a shape: pick_schedule)
     const int* sched = nullptr;
-    if (STRIP && !SIG && slots > 0 && env_int("STENCIL_BOXK_PACK", sizeof(T) == 8 ? 1 : 0) && !(lo || hi)) {
+    std::atomic<int>* verdict = nullptr;
+    const int64_t nb_equal = nb;
+    const int pack_mode = env_int("STENCIL_BOXK_PACK", sizeof(T) == 8 ? 1 : 0);
+    if (STRIP && !SIG && slots > 0 && pack_mode && !(lo || hi)) {
         int dev = 0;
         STENCIL_HIP_CHECK(hipGetDevice(&dev));
-        if (const int rc = packed_schedule(1, dev, tiles, nz, K, 3 * K, slots, zc, &sched, &nb)) return rc;
+        if (const int rc = packed_schedule(1, dev, tiles, nz, K, 3 * K, slots, zc, &sched, &nb, &verdict)) return rc;
+        if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
+        if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
-    hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
-                       static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig, sched);
-    STENCIL_LAUNCH_CHECK();
+    auto launch = [&](bool packed) {
+        hipLaunchKernelGGL(kern, dim3(unsigned(packed ? nb : nb_equal)), dim3(64, NW, 1), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
+                           int(gy), int(lo), int(hi), int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig,
+                           packed ? sched : nullptr);
+        return hipGetLastError();
+    };
+    if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
+    if (const hipError_t e = launch(sched != nullptr); e != hipSuccess)
+        return set_error(STENCIL_EHIP, "kernel launch failed: %s (box)", hipGetErrorString(e));
     return STENCIL_OK;
 }
 

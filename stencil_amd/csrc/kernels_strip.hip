@@ -38,7 +38,9 @@
 // value; slab-halo planes (HALO_LO/HI) are advanced.  Bitwise equal to K
 // plain sweeps (tests/test_gpu_parity.py).
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -484,20 +486,27 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (nsig) *nsig = int(tiles);
     }
     const int* sched = nullptr;
-    // default: the packed longest-first schedule when it beats equal chunks
-    // (512^3 fp64 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a
-    // multi-GPU job, whose one-round grid above is deliberate
-    if (!SIG && zc > 0 && senv_int("STENCIL_TK_PACK", 1) && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
+    std::atomic<int>* verdict = nullptr;
+    const int64_t nb_equal = nb;
+    // default: the packed longest-first schedule where the model predicts a
+    // gain AND the first launch measured it faster (pick_schedule; 512^3 fp64
+    // 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a multi-GPU
+    // job, whose one-round grid above is deliberate
+    const int pack_mode = senv_int("STENCIL_TK_PACK", 1);
+    if (!SIG && zc > 0 && pack_mode && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
         !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
-        const int rc = packed_schedule(0, dev, gx * gy, nz, K, 2 * K, slots, zc, &sched, &nb);
+        const int rc = packed_schedule(0, dev, gx * gy, nz, K, 2 * K, slots, zc, &sched, &nb, &verdict);
         if (rc != STENCIL_OK) return rc;
+        if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
+        if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
     // interior steps without ghost-cell selects (fp64 one-cell-per-lane shapes):
     // by default only where the packed schedule runs -- few tiles, 512^3 fp64
     // 1212 vs 1175 Gcell/s -- since on large planes the duplicated step loses
     // (2048^2 x 512 1357 vs 1384, 2048^3 1310 vs 1365; profiles/r02o_ab_tk_fast.log)
-    const int fast = senv_int("STENCIL_TK_FAST", sched != nullptr ? 1 : 0);
+    const int fast_env = senv_int("STENCIL_TK_FAST", -1);
+    auto fast_of = [&](bool packed) { return fast_env >= 0 ? fast_env : (packed ? 1 : 0); };
     if (senv_int("STENCIL_TK_VERBOSE", 0)) {
         int per_cu = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0);
@@ -515,10 +524,16 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         info->steps = K;
         return STENCIL_OK;
     }
-    hipLaunchKernelGGL(kern, dim3(unsigned(nb)), dim3(64, NW, 1), 0, s, static_cast<const T*>(in),
-                       static_cast<T*>(out), g, int(begin), int(end), zc, int(gx), int(gy), int(lo), int(hi),
-                       avg_weight<T>(l.prob), sig, fsig, sched, fast);
-    STENCIL_LAUNCH_CHECK();
+    auto launch = [&](bool packed) {
+        hipLaunchKernelGGL(kern, dim3(unsigned(packed ? nb : nb_equal)), dim3(64, NW, 1), 0, s,
+                           static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
+                           int(gy), int(lo), int(hi), avg_weight<T>(l.prob), sig, fsig, packed ? sched : nullptr,
+                           fast_of(packed));
+        return hipGetLastError();
+    };
+    if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
+    if (const hipError_t e = launch(sched != nullptr); e != hipSuccess)
+        return set_error(STENCIL_EHIP, "kernel launch failed: %s (tkstrip)", hipGetErrorString(e));
     return STENCIL_OK;
 }
 
@@ -553,14 +568,20 @@ static int64_t simulate_makespan(const std::vector<int>& len, int fill, int slot
 // keyed by device ordinal and guarded (a process may drive several GPUs from
 // several threads: stencil_set_device is per thread).
 int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    const int** sched, int64_t* nb) {
+                    const int** sched, int64_t* nb, std::atomic<int>** verdict) {
     // Only grids of few tiles: with more than 2 tiles per slot the equal
     // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
     // Gcell/s), and the search would cost host time at the first launch.
     if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
     if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
+    struct Entry {
+        int* table = nullptr;
+        int64_t workgroups = 0;
+        std::atomic<int> verdict{kPackUntested};
+    };
     static std::mutex mu;
-    static std::map<std::tuple<int, int, int64_t, int64_t, int, int>, std::pair<int*, int64_t>> cache;
+    // map nodes never move: the verdict's address stays valid for the process
+    static std::map<std::tuple<int, int, int64_t, int64_t, int, int>, Entry> cache;
     std::lock_guard<std::mutex> lock(mu);
     const auto key = std::make_tuple(family, dev, tiles, nz, K, slots);
     auto hit = cache.find(key);
@@ -604,12 +625,47 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
         if (senv_int("STENCIL_TK_VERBOSE", 0))
             std::fprintf(stderr, "pack (family %d): equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n", family,
                          (long long)base, (long long)best, (long long)n, d ? "" : " -- not used");
-        hit = cache.emplace(key, std::make_pair(d, n)).first;
+        hit = cache.try_emplace(key).first;
+        hit->second.table = d;
+        hit->second.workgroups = n;
     }
-    if (hit->second.first) {
-        *sched = hit->second.first;
-        *nb = hit->second.second;
+    if (hit->second.table) {
+        *sched = hit->second.table;
+        *nb = hit->second.workgroups;
+        if (verdict) *verdict = &hit->second.verdict;
     }
+    return STENCIL_OK;
+}
+
+int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<hipError_t(bool)>& launch) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    STENCIL_HIP_CHECK(hipStreamIsCapturing(s, &cap));
+    if (cap != hipStreamCaptureStatusNone) {  // no host sync inside a capture: the model's choice
+        STENCIL_HIP_CHECK(launch(true));
+        return STENCIL_OK;
+    }
+    constexpr int kRounds = 3;
+    hipEvent_t ev[2 * kRounds + 1];
+    for (auto& e : ev) STENCIL_HIP_CHECK(hipEventCreate(&e));
+    hipError_t err = hipEventRecord(ev[0], s);
+    for (int i = 0; i < 2 * kRounds && err == hipSuccess; ++i) {
+        err = launch(i % 2 == 0);  // packed, equal, packed, ...
+        if (err == hipSuccess) err = hipEventRecord(ev[i + 1], s);
+    }
+    if (err == hipSuccess) err = hipEventSynchronize(ev[2 * kRounds]);
+    float best[2] = {1e30f, 1e30f};
+    for (int i = 0; i < 2 * kRounds && err == hipSuccess; ++i) {
+        float ms = 0.f;
+        err = hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+        best[i % 2] = std::min(best[i % 2], ms);
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (err != hipSuccess)
+        return set_error(STENCIL_EHIP, "schedule trial failed: %s", hipGetErrorString(err));
+    verdict->store(best[0] < best[1] ? kPackPacked : kPackEqual);
+    if (senv_int("STENCIL_TK_VERBOSE", 0))
+        std::fprintf(stderr, "schedule trial: packed %.4f ms, equal chunks %.4f ms -> %s\n", best[0], best[1],
+                     best[0] < best[1] ? "packed" : "equal chunks");
     return STENCIL_OK;
 }
 

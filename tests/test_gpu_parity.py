@@ -335,6 +335,33 @@ def test_tkstrip_packed_schedule_small_shapes(gpu, dtype):
     assert any(packed), list(zip(shapes, packed))
 
 
+@pytest.mark.parametrize("shape", ["star", "box"])
+@pytest.mark.parametrize("mode", ["1", "2", "0"])
+def test_schedule_choice_modes(gpu, monkeypatch, shape, mode):
+    """Packed vs equal z-chunks (kernels_strip.hip pick_schedule): mode 1 (the
+    default) times both grids on the first launch of a shape and keeps the
+    faster -- six trial launches, all writing the same output; mode 2 launches
+    the dispatcher model's choice unmeasured (packed here); mode 0 equal chunks.
+    256^3 fp64 is a shape the model packs (and where the measured choice is
+    equal chunks on MI355X, profiles/r02gg_pack.log).  Every mode bitwise
+    against the oracle, over two launches (the trial, then the verdict)."""
+    monkeypatch.setenv("STENCIL_TK_PACK", mode)
+    monkeypatch.setenv("STENCIL_BOXK_PACK", mode)
+    nx = ny = nz = 256
+    e = engine(gpu, 3, "fp64", shape, 1, "naive", "auto", nx, ny, nz)
+    k = e.fuse_steps
+    if shape == "star":
+        assert e.sweepk_geometry(k)["packed"] == (mode != "0")  # before any launch: the model's plan
+    it = 2 * k + 1
+    p = ob.problem(3, "fp64", shape, 1, "naive", nx, ny, nz)
+    want = ob.run(p, it, "random", 19, threads=16)
+    e.reset("random", 19)
+    fin, _ = e.iterate(it)
+    assert same_bits(e.to_numpy(fin), want)
+    if shape == "star" and mode == "2":
+        assert e.sweepk_geometry(k)["packed"]
+
+
 @pytest.mark.parametrize("cfg", ["default", "216", "408", "308", "208", "10116", "10216", "20116"])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
@@ -601,6 +628,8 @@ def test_benched_kernel_at_benched_shape(gpu, case):
         assert geo["packed"] == packed, geo
     e.reset("random", 4242)
     fin, _ = e.iterate(it)
+    if packed:  # the first launch timed both grids (pick_schedule): at 512^3 packed wins by ~8 %
+        assert e.sweepk_geometry(k)["packed"], "measured choice at the C2 shape: equal chunks"
     got = e.interior(fin).cpu().numpy()
     del e, fin
     torch.cuda.empty_cache()
