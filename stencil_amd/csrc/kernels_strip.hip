@@ -581,9 +581,12 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
     };
     static std::mutex mu;
     // map nodes never move: the verdict's address stays valid for the process
-    static std::map<std::tuple<int, int, int64_t, int64_t, int, int>, Entry> cache;
+    static std::map<std::tuple<int, int, int64_t, int64_t, int, int, int>, Entry> cache;
     std::lock_guard<std::mutex> lock(mu);
-    const auto key = std::make_tuple(family, dev, tiles, nz, K, slots);
+    // STENCIL_TK_PACK_LC (experiments): chunks of exactly this many planes,
+    // used whatever the model says
+    const int force_lc = senv_int("STENCIL_TK_PACK_LC", 0);
+    const auto key = std::make_tuple(family, dev, tiles, nz, K, slots, force_lc);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
         auto build = [&](int64_t lc, std::vector<int>& tab) {
@@ -607,9 +610,13 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
         std::vector<int> tab, best_tab;
         const int64_t base = build(zc, tab);
         int64_t best = base;
-        for (int64_t lc = std::max<int64_t>(fill, nz / 16); lc <= nz; lc += std::max<int64_t>(1, nz / 256)) {
+        for (int64_t lc = std::max<int64_t>(fill, nz / 16); lc <= nz && force_lc <= 0; lc += std::max<int64_t>(1, nz / 256)) {
             const int64_t m = build(lc, tab);
             if (m < best) best = m, best_tab = tab;
+        }
+        if (force_lc > 0) {
+            build(force_lc, best_tab);
+            best = -1;  // always used
         }
         int* d = nullptr;
         int64_t n = 0;
