@@ -646,7 +646,10 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
 
 int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<hipError_t(bool)>& launch) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    STENCIL_HIP_CHECK(hipStreamIsCapturing(s, &cap));
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+        (void)hipGetLastError();  // status unknown: do not block, launch untimed
+        cap = hipStreamCaptureStatusActive;
+    }
     if (cap != hipStreamCaptureStatusNone) {  // no host sync inside a capture: the model's choice
         STENCIL_HIP_CHECK(launch(true));
         return STENCIL_OK;
