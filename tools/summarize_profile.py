@@ -4,9 +4,12 @@ bench's traffic table profiles/traffic.json.
 
 HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes: rocprofv3
 reports both in KiB, and on gfx950 FETCH_SIZE counts exactly half the bytes of
-wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md §HBM) -- the
-stencil kernels' loads are all global_load_dwordx4, so the factor 2 applies
-(calibrated in the same run by the copy kernel: 1 GiB read, FETCH_SIZE = 512 MiB).
+wide coalesced streaming reads (MI355X_MICROARCH.md §HBM: FETCH_SIZE = RDREQ x 64 B
+while the requests are 128 B) -- the strip kernels' reads are all 128-B requests
+(RDREQ_128B = RDREQ), whatever their lane width (8 B fp64 V = 1,
+16 B otherwise), so the factor 2 applies; calibrated in the same run by the copy
+kernel (1 GiB read, FETCH_SIZE = 512 MiB), and without it the fp64 strip kernel's
+reads would fall below the compulsory 1.07 GB per 512^3 launch.
 usage: python tools/summarize_profile.py <tag> [workload-key]"""
 import collections
 import csv
