@@ -237,6 +237,14 @@ int stencil_wait_face_signal(const uint64_t* face_signal, uint64_t target, void*
 int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iterations, void* stream,
                     int* final_in_b, float* elapsed_ms);
 
+/* Settle stencil_iterate's one-time, per-shape choices before a timed run:
+ * the first fused launch of the job (K-step 7-point star or box) from `a`
+ * into `b`, which on a shape's first use times the packed and equal z-chunk
+ * grids (blocking once) and keeps the faster.  `a` is not changed; `b` is
+ * overwritten (its ghost cells are not).  A no-op for jobs without a K-step
+ * launch.  No reference counterpart (the reference has no per-shape state). */
+int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream);
+
 /* Launch plan of stencil_iterate for `iterations`: number of kernel launches
  * and the kernel family AUTO resolves to. */
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches,

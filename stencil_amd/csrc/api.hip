@@ -624,6 +624,23 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
     return STENCIL_OK;
 }
 
+int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (!a || !b || a == b) return set_error(STENCIL_EINVAL, "need two distinct grids");
+    hipStream_t s = as_stream(stream);
+    const int64_t n = stencil_slow_extent(l);
+    int rc = STENCIL_OK;
+    if (iterate_persistent(l->prob) || iterate_tb2d(l->prob)) {
+        // 2D jobs: nothing is chosen per shape at run time
+    } else if (const int k = iterate_tk_steps(l->prob)) {
+        rc = launch_temporalk(*l, a, b, 0, n, k, s);
+    } else if (const int k = iterate_box_steps(l->prob)) {
+        rc = launch_boxk(*l, a, b, 0, n, k, s);
+    }
+    if (rc == STENCIL_OK) clear_error();
+    return rc;
+}
+
 int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iterations, void* stream, int* final_in_b,
                     float* elapsed_ms) {
     if (int rc = check_layout(l)) return rc;

@@ -194,6 +194,9 @@ auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGri
     if (options.iterations > 0) {
         int fin = 0;
         check(stencil_iterate(&l, d.a, d.b, 1, nullptr, &fin, nullptr), "warm-up");
+        // and the per-shape z-chunk schedule choice, timed on a shape's first
+        // fused launch (kernels_strip.hip pick_schedule)
+        check(stencil_prepare(&l, d.a, d.b, nullptr), "warm-up");
         upload(d.a, matrix);
         upload(d.b, result);
         check(stencil_synchronize(nullptr), "synchronize");

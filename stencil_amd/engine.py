@@ -167,6 +167,13 @@ class JacobiEngine:
                    "stencil_iterate")
         return (self.b if fin.value else self.a), (ms.value if timed else None)
 
+    def prepare(self, stream=None) -> None:
+        """stencil_prepare: settle the job's one-time per-shape choices (the
+        z-chunk schedule trial) by one fused launch a -> b; `a` is unchanged."""
+        _lib.check(self.lib.stencil_prepare(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
+                                            ctypes.c_void_p(self.b.data_ptr()), _stream_handle(stream)),
+                   "stencil_prepare")
+
     def plan(self, iterations: int):
         launches = ctypes.c_int64(0)
         kernel = ctypes.c_int32(0)
