@@ -655,9 +655,11 @@ int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<
         return STENCIL_OK;
     }
     constexpr int kRounds = 3;
-    hipEvent_t ev[2 * kRounds + 1];
-    for (auto& e : ev) STENCIL_HIP_CHECK(hipEventCreate(&e));
-    hipError_t err = hipEventRecord(ev[0], s);
+    hipEvent_t ev[2 * kRounds + 1] = {};
+    hipError_t err = hipSuccess;
+    for (auto& e : ev)
+        if (err == hipSuccess) err = hipEventCreate(&e);
+    if (err == hipSuccess) err = hipEventRecord(ev[0], s);
     for (int i = 0; i < 2 * kRounds && err == hipSuccess; ++i) {
         err = launch(i % 2 == 0);  // packed, equal, packed, ...
         if (err == hipSuccess) err = hipEventRecord(ev[i + 1], s);
@@ -669,7 +671,8 @@ int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<
         err = hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
         best[i % 2] = std::min(best[i % 2], ms);
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
     if (err != hipSuccess)
         return set_error(STENCIL_EHIP, "schedule trial failed: %s", hipGetErrorString(err));
     verdict->store(best[0] < best[1] ? kPackPacked : kPackEqual);
