@@ -245,6 +245,17 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
  * launch.  No reference counterpart (the reference has no per-shape state). */
 int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream);
 
+/* The dispatcher model behind the packed z-chunk schedule, on the host (no
+ * GPU needed): `tiles` x-y tiles of `planes` planes on `slots` one-workgroup
+ * CU slots, `fill` planes of pipeline fill per chunk (2K for the 7-point
+ * K-step kernel, 3K for the box), equal chunks of `zchunk` planes as the
+ * alternative.  Returns the simulated makespans (plane steps) of the equal
+ * chunks and of the best packed grid, and the packed grid's workgroups (0 when
+ * it would not be used: it must beat equal chunks by 2 %).  stencil_iterate
+ * then times both grids on a shape's first launch (STENCIL_TK_PACK=1). */
+int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,
+                      int64_t* equal_steps, int64_t* packed_steps, int64_t* workgroups);
+
 /* Launch plan of stencil_iterate for `iterations`: number of kernel launches
  * and the kernel family AUTO resolves to. */
 int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches,

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "stencil_layout_init", "stencil_slow_extent", "stencil_device_count", "stencil_set_device",
     "stencil_synchronize", "stencil_alloc", "stencil_free", "stencil_fill_initial", "stencil_upload",
     "stencil_download", "stencil_copy_planes", "stencil_sweep", "stencil_sweep2", "stencil_sweepk", "stencil_iterate",
-    "stencil_prepare", "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth", "stencil_sweepk_geometry", "stencil_sweepk_signal",
+    "stencil_prepare", "stencil_pack_plan", "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth", "stencil_sweepk_geometry", "stencil_sweepk_signal",
     "stencil_wait_counters", "stencil_face_signal_create", "stencil_face_signal_destroy",
     "stencil_face_signal_reset", "stencil_face_signal_read", "stencil_wait_face_signal",
     "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
@@ -107,6 +107,8 @@ def load() -> ctypes.CDLL:
         "stencil_sweepk": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
         "stencil_iterate": (c_int, [L, c_void_p, c_void_p, c_uint32, c_void_p, POINTER(c_int), POINTER(c_float)]),
         "stencil_prepare": (c_int, [L, c_void_p, c_void_p, c_void_p]),
+        "stencil_pack_plan": (c_int, [c_int64, c_int64, c_int32, c_int32, c_int32, POINTER(c_int64),
+                                      POINTER(c_int64), POINTER(c_int64)]),
         "stencil_plan": (c_int, [L, c_uint32, POINTER(c_int64), POINTER(c_int32)]),
         "stencil_plane_sums": (c_int, [L, c_void_p, POINTER(c_double), c_void_p]),
         "stencil_copy_bandwidth": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, POINTER(c_float)]),

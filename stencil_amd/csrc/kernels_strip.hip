@@ -558,6 +558,47 @@ static int64_t simulate_makespan(const std::vector<int>& len, int fill, int slot
     return span;
 }
 
+// The dispatcher-model search behind packed_schedule (host only): chunks of
+// Lc planes per tile, longest first, for every Lc in [max(fill, nz/16), nz];
+// *base = the simulated makespan of equal chunks of zc planes, *best the best
+// packed one (force_lc > 0: that Lc, *best = -1), *tab its {tile, first
+// plane, planes} table (empty when no Lc beats equal chunks).
+static void pack_search(int64_t tiles, int64_t nz, int fill, int slots, int zc, int force_lc, std::vector<int>* tab_out,
+                        int64_t* base_out, int64_t* best_out) {
+    auto build = [&](int64_t lc, std::vector<int>& tab) {
+        lc = std::max<int64_t>(1, lc);
+        struct Item { int len, c, t, z; };
+        std::vector<Item> items;
+        for (int64_t t = 0; t < tiles; ++t)
+            for (int64_t z = 0, c = 0; z < nz; z += lc, ++c)
+                items.push_back({int(std::min<int64_t>(lc, nz - z)), int(c), int(t), int(z)});
+        std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+            return a.len != b.len ? a.len > b.len : (a.c != b.c ? a.c < b.c : a.t < b.t);
+        });
+        std::vector<int> len;
+        tab.clear();
+        for (const Item& it : items) {
+            len.push_back(it.len);
+            tab.insert(tab.end(), {it.t, it.z, it.len});
+        }
+        return simulate_makespan(len, fill, slots);
+    };
+    std::vector<int> tab, best_tab;
+    const int64_t base = build(zc, tab);
+    int64_t best = base;
+    for (int64_t lc = std::max<int64_t>(fill, nz / 16); lc <= nz && force_lc <= 0; lc += std::max<int64_t>(1, nz / 256)) {
+        const int64_t m = build(lc, tab);
+        if (m < best) best = m, best_tab = tab;
+    }
+    if (force_lc > 0) {
+        build(force_lc, best_tab);
+        best = -1;  // always used
+    }
+    *tab_out = std::move(best_tab);
+    *base_out = base;
+    *best_out = best;
+}
+
 // STENCIL_TK_PACK (default 1; 0 = equal chunks): chunks of Lc planes per tile (the last one
 // shorter), longest first -- every tile's full chunks start in z lock-step,
 // the short remainders fill the CUs the full chunks leave idle.  Lc is the
@@ -589,35 +630,9 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
     const auto key = std::make_tuple(family, dev, tiles, nz, K, slots, force_lc);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
-        auto build = [&](int64_t lc, std::vector<int>& tab) {
-            lc = std::max<int64_t>(1, lc);
-            struct Item { int len, c, t, z; };
-            std::vector<Item> items;
-            for (int64_t t = 0; t < tiles; ++t)
-                for (int64_t z = 0, c = 0; z < nz; z += lc, ++c)
-                    items.push_back({int(std::min<int64_t>(lc, nz - z)), int(c), int(t), int(z)});
-            std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
-                return a.len != b.len ? a.len > b.len : (a.c != b.c ? a.c < b.c : a.t < b.t);
-            });
-            std::vector<int> len;
-            tab.clear();
-            for (const Item& it : items) {
-                len.push_back(it.len);
-                tab.insert(tab.end(), {it.t, it.z, it.len});
-            }
-            return simulate_makespan(len, fill, slots);
-        };
-        std::vector<int> tab, best_tab;
-        const int64_t base = build(zc, tab);
-        int64_t best = base;
-        for (int64_t lc = std::max<int64_t>(fill, nz / 16); lc <= nz && force_lc <= 0; lc += std::max<int64_t>(1, nz / 256)) {
-            const int64_t m = build(lc, tab);
-            if (m < best) best = m, best_tab = tab;
-        }
-        if (force_lc > 0) {
-            build(force_lc, best_tab);
-            best = -1;  // always used
-        }
+        std::vector<int> best_tab;
+        int64_t base = 0, best = 0;
+        pack_search(tiles, nz, fill, slots, zc, force_lc, &best_tab, &base, &best);
         int* d = nullptr;
         int64_t n = 0;
         if (!best_tab.empty() && best * 50 < base * 49) {
@@ -777,3 +792,21 @@ int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, in
 }
 
 }  // namespace stencil
+
+// The packed-schedule model on the host, without a GPU (tests, tools): see
+// include/stencil_hip.h.
+int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk, int64_t* equal_steps,
+                      int64_t* packed_steps, int64_t* workgroups) {
+    using namespace stencil;
+    if (tiles <= 0 || planes <= 0 || fill < 0 || slots <= 0 || zchunk <= 0 || planes > (int64_t(1) << 30) ||
+        tiles * ((planes + zchunk - 1) / zchunk) > (int64_t(1) << 26))
+        return set_error(STENCIL_EINVAL, "pack plan: tiles, planes, slots, zchunk > 0, fill >= 0, at most 2^26 chunks");
+    std::vector<int> tab;
+    int64_t base = 0, best = 0;
+    pack_search(tiles, planes, fill, slots, zchunk, 0, &tab, &base, &best);
+    if (equal_steps) *equal_steps = base;
+    if (packed_steps) *packed_steps = best;
+    if (workgroups) *workgroups = (!tab.empty() && best * 50 < base * 49) ? int64_t(tab.size() / 3) : 0;
+    clear_error();
+    return STENCIL_OK;
+}
