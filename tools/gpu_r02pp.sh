@@ -1,6 +1,8 @@
 #!/bin/bash
 # Box K=4 with E pinned (4 x 8 and 2 x 16 rows, both spill 21-30 VGPRs) against
 # the default 3 x 8 K=4 strip: per-sweep time, interleaved in one process
+# (the pinned variants, cfg 980xxx, were removed after this measurement: the
+# script now times the default shape only)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
