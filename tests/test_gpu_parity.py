@@ -555,7 +555,9 @@ def test_full_size_c2_bitwise_few_iterations(gpu):
 def test_full_size_c2_1000_iterations_properties(gpu):
     """The whole config-2 job (1000 sweeps, reference initial condition):
     ghost cells untouched, bitwise x-mirror symmetry (0+L+R == 0+R+L), all
-    values in [0, 1], plane checksums identical across kernel families."""
+    values in [0, 1], plane checksums identical across kernel families --
+    AUTO (the benched K = 4 strip launches), the single-sweep z-march and the
+    direct kernel, whole grids bitwise equal."""
     import torch
     n = 512
     e = engine(gpu, 3, "fp64", "star", 1, "naive", "zmarch", n, n, n)
@@ -570,11 +572,61 @@ def test_full_size_c2_1000_iterations_properties(gpu):
     mask[1:-1, 1:-1, 1:-1] = False
     assert torch.equal(g[mask], init[mask])
     sums_zm = e.plane_sums(fin)
-    e2 = engine(gpu, 3, "fp64", "star", 1, "naive", "direct", n, n, n)
-    e2.reset()
-    fin2, _ = e2.iterate(1000)
-    assert np.array_equal(sums_zm, e2.plane_sums(fin2))
-    assert torch.equal(e2.interior(fin2), inner)
+    for kernel in ("direct", "auto"):
+        e2 = engine(gpu, 3, "fp64", "star", 1, "naive", kernel, n, n, n)
+        e2.reset()
+        fin2, _ = e2.iterate(1000)
+        assert np.array_equal(sums_zm, e2.plane_sums(fin2)), kernel
+        assert torch.equal(e2.interior(fin2), inner), kernel
+        del e2, fin2
+    torch.cuda.empty_cache()
+
+
+def test_c2_whole_benched_job_against_oracle(gpu):
+    """The headline job exactly as bench.py times it -- BASELINE config 2,
+    512^3 fp64 7-point from the reference initial condition, 1000 sweeps
+    through AUTO = 250 K = 4 strip launches on the packed schedule the first
+    launch measured faster -- bitwise against the oracle's naive loop
+    (stencil.cpp:94-131 generalised to 3D, multithreaded, same per-cell
+    arithmetic) over the WHOLE job, not a few sweeps."""
+    import torch
+    from stencil_amd import _lib
+    n, it = 512, 1000
+    e = engine(gpu, 3, "fp64", "star", 1, "naive", "auto", n, n, n)
+    assert e.fuse_steps == 4
+    assert e.plan(it) == (250, _lib.KERNEL_TEMPORALK)
+    e.reset()
+    e.prepare()  # bench.py settles the schedule first; grid a is unchanged
+    fin, _ = e.iterate(it)
+    assert e.sweepk_geometry(4)["packed"], "the measured choice at the C2 shape is packed (bench.py's launch)"
+    got = e.interior(fin).cpu().numpy()
+    del e, fin
+    torch.cuda.empty_cache()
+    p = ob.problem(3, "fp64", "star", 1, "naive", n, n, n)
+    want = ob.interior(p, ob.run(p, it, threads=16))
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
+    # the diffusion fronts have reached every cell, so the job is not trivially zero anywhere
+    assert float(want.min()) > 0.0
+
+
+def test_c5_slab_reference_job_against_oracle(gpu):
+    """One GPU's slab of BASELINE config 5 (2048^2 x 256 27-point box, fp64)
+    from the reference initial condition, 12 sweeps through AUTO = three K = 4
+    box strip launches (the benched kernel), bitwise against the oracle."""
+    import torch
+    from stencil_amd import _lib
+    nx, ny, nz, it = 2048, 2048, 256, 12
+    e = engine(gpu, 3, "fp64", "box", 1, "naive", "auto", nx, ny, nz)
+    assert e.fuse_steps == 4
+    assert e.plan(it) == (3, _lib.KERNEL_TEMPORAL2)
+    e.reset()
+    fin, _ = e.iterate(it)
+    got = e.interior(fin).cpu().numpy()
+    del e, fin
+    torch.cuda.empty_cache()
+    p = ob.problem(3, "fp64", "box", 1, "naive", nx, ny, nz)
+    want = ob.interior(p, ob.run(p, it, threads=16))
+    assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
 
 
 @pytest.mark.parametrize("cfg", ["C5_slab_box_fp64", "C4_slab_fp64", "C3_fp32_4096sq"])
