@@ -13,21 +13,37 @@ HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fno-gpu-flush-denormals-to-zero -Wall -Wno-pass-failed -Iinclude -Istencil_amd/csrc
 CXXFLAGS ?= -O2 -std=c++17 -Wall -Wextra -ffp-contract=off -Iinclude
 
+# The product library and its debug twin: the same kernel objects, linked
+# with knobs.cpp built without / with -DSTENCIL_DEBUG_KNOBS (the debug library
+# reads the experiment knobs -- workgroup shapes, forced z-chunks -- from the
+# environment; the product runs AUTO's plan only).
 LIB := stencil_amd/libstencil_hip.so
+LIB_DBG := stencil_amd/libstencil_hip_debug.so
 CLI := build/bin/stencil_main
 SRCS := $(wildcard stencil_amd/csrc/*.hip)
 OBJS := $(patsubst stencil_amd/csrc/%.hip,build/obj/%.o,$(SRCS))
 HOST_SRCS := $(wildcard stencil_amd/csrc/host/*.cpp)
 HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
 
-all: $(LIB) $(CLI) oracle
+all: $(LIB) $(LIB_DBG) $(CLI) oracle
 
 build/obj/%.o: stencil_amd/csrc/%.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
 	@mkdir -p build/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+build/obj/knobs.o: stencil_amd/csrc/knobs.cpp
+	@mkdir -p build/obj
+	$(CXX) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
+
+build/obj/knobs_debug.o: stencil_amd/csrc/knobs.cpp
+	@mkdir -p build/obj
+	$(CXX) -O2 -std=c++17 -fPIC -Wall -DSTENCIL_DEBUG_KNOBS -c $< -o $@
+
+$(LIB): $(OBJS) build/obj/knobs.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) build/obj/knobs.o
+
+$(LIB_DBG): $(OBJS) build/obj/knobs_debug.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) build/obj/knobs_debug.o
 
 $(CLI): $(HOST_SRCS) $(HOST_HDRS) $(LIB) include/stencil_hip.h
 	@mkdir -p build/bin
@@ -38,7 +54,7 @@ oracle:
 	bash oracle/ref/build.sh
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(LIB_DBG)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: 3D 7-point fp64 Jacobi (BASELINE.json metric, config 2 size per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|NS]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Two multi-GPU drivers, same job, same JSON line:
+  * one process per GPU (launched by torch.distributed.run; WORLD_SIZE set):
+    stencil_amd/slab.py over torch.distributed (RCCL);
+  * --gpus N without a launcher (WORLD_SIZE unset): ONE process drives the N
+    GPUs through the C-ABI slab job (stencil_slab_*, csrc/slab.hip; RCCL
+    ncclCommInitAll), the shape of the reference's single spawn/join of its
+    whole decomposed job (src/stencil/stencil.cpp:34-53).
 
 --config picks another BASELINE.json config as the workload (C3: 4096^3 fp32,
 C4: 2048x2048x4096 fp64, C5: 2048^3 27-point fp64), its global grid z-slab
@@ -44,7 +52,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH
 PRESETS = {
     "C2": dict(dtype="fp64", shape="star", grid=None, min_gpus=1,
                desc="BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU"),
-    "C3": dict(dtype="fp32", shape="star", grid=(4096, 4096, 4096), min_gpus=2,
+    # C3 on one GPU: ONE resident grid + a rolling margin (stencil_rolling_*),
+    # since two grids are 2 x 279 GB
+    "C3": dict(dtype="fp32", shape="star", grid=(4096, 4096, 4096), min_gpus=1,
                desc="BASELINE config 3: 3D 7-point fp32 Jacobi, 4096^3"),
     "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=2,
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
@@ -91,10 +101,11 @@ def parse():
                     help="multi-GPU rounds as separate boundary/interior launches (no face counters)")
     ap.add_argument("--face-signal", action="store_true",
                     help="face-signalled rounds gated by hipStreamWaitValue64 on a signal word, not the wait kernel")
-    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self"],
-                    help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only)")
+    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self", "copy"],
+                    help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only); "
+                         "without a launcher, copy = device copies between the slabs (hipMemcpyPeerAsync)")
     ap.add_argument("--share-device", action="store_true",
-                    help="rehearsal: every rank uses GPU 0 (needs --exchange host)")
+                    help="rehearsal: every rank / slab uses GPU 0 (needs --exchange host, or copy without a launcher)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
@@ -205,6 +216,8 @@ def main():
     from stencil_amd.slab import (HostStagedExchanger, LoopbackExchanger, SelfP2PExchanger, SlabInfo, SlabJacobi,
                                   TorchDistExchanger, partition)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return main_slab_job(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -240,99 +253,118 @@ def main():
     else:                    # strong scaling: the global grid split in z-slabs
         gnx, gny, gnz = pre["grid"]
         first, count = partition(gnz, world, rank)
-    # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
-    # 4 for the 7-point star, 3 or 4 for the box) so K sweeps fuse across the
-    # exchange too (one K-plane exchange per K-sweep round).
+    # C3 on one GPU: two grids do not fit (2 x 279 GB); ONE resident grid plus
+    # a rolling margin of spare planes (stencil_rolling_*, bitwise the
+    # two-grid job), the margin as deep as the free HBM allows
+    rolling = args.config == "C3" and world == 1 and not loop
     spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
-    fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps
-    if world > 1 or loop:
-        spec = dataclasses.replace(spec, halo=max(2, fuse))
-    flags = (_lib.HALO_LO if rank > 0 or loop else 0) | (_lib.HALO_HI if rank < world - 1 or loop else 0)
-    eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
-    if loop:
-        exchanger = LoopbackExchanger() if args.exchange == "loopback" else SelfP2PExchanger(0, 1)
-        info = SlabInfo(0, 3, first, count)  # drives the multi-rank round structure
-    else:
-        exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
-        info = SlabInfo(rank, world, first, count)
-    SlabJacobi.use_signal = not args.no_signal
-    SlabJacobi.use_face_signal = args.face_signal
-    slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
-    slab.init("reference")
-    kernel_id = eng.plan(12)[1]
-    kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
-    if spec.shape == "box" and kname in ("temporal2", "temporalk"):
-        kname = "boxk"  # the box's fused family (kernels_boxk.hip)
     multi = world > 1 or loop  # the slab round structure (exchange + two streams)
-    sweeps_per_launch = eng.fuse_steps if not multi else slab.launches_per_round()
+    extra = 0
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---------------- warmup
-    if not multi:
-        # settle the one-time per-shape choice (packed vs equal z-chunks, timed
-        # on the first launch of a shape) outside the timed region whatever W
-        # is: one fused launch a -> b, grid a unchanged
-        eng.prepare()
-        eng.iterate(args.warmup)
-    else:
-        slab.run(args.warmup)
-    barrier()
-
-    # ---------------- timed region: exactly K sweeps
-    stream = torch.cuda.current_stream()
-    t0 = time.perf_counter()
-    if not multi:
-        _, dev_ms = eng.iterate(args.steps, stream=stream, timed=True)
+    if rolling:
+        from stencil_amd.engine import RollingGrid
+        free = torch.cuda.mem_get_info(local)[0]
+        plane_b = RollingGrid.bytes_needed(spec, gnx, gny, 1, 64) - RollingGrid.bytes_needed(spec, gnx, gny, 1, 63)
+        need = RollingGrid.bytes_needed(spec, gnx, gny, gnz, 8)
+        shift = int(min(512, (free - need - (2 << 30)) // plane_b + 8))
+        if shift < 16:
+            raise SystemExit(f"--config C3 on one GPU needs {need / 2**30:.0f} GiB + a margin; {free / 2**30:.0f} GiB free")
+        grid = RollingGrid(spec, gnx, gny, gnz, shift, device=local)
+        grid.reset("reference")
+        kname = "temporalk"
+        sweeps_per_launch = grid.sweeps_per_pass
+        grid.iterate(args.warmup)
+        barrier()
+        t0 = time.perf_counter()
+        _, dev_ms, kernel_launches = grid.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
         kernel_ms_total = dev_ms
-        kernel_launches = eng.plan(args.steps)[0]
+        cells_per_launch = float(gnx) * gny * gnz  # charged per pass of K sweeps over the whole grid
+        rolling_info = {"shift_planes": shift, "launch_planes": shift - sweeps_per_launch,
+                        "launches": kernel_launches, "grid_bytes": grid.bytes}
     else:
-        slab.run(args.steps)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.exchange == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-    if multi and slab.signal_timeouts():
-        raise SystemExit("a face-counter wait timed out: the slab rounds did not complete")
-    if multi:
-        # Interior launch time for the roofline, from HIP events on the
-        # interior stream over a few more rounds AFTER the timed region: the
-        # events are extra queue packets (~5 us each per round on MI355X) that
-        # the timed rounds do not carry.
-        slab.start_kernel_timing()
-        extra = max(4, min(args.steps, 8)) * slab.launches_per_round()
-        slab.run(extra)
-        kernel_ms_total, kernel_launches = slab.stop_kernel_timing()
-        if world > 1:
-            dist.barrier()
-    check = None
-    if world > 1 and not args.no_check:
-        check = verify_slabs(eng, slab, spec, (gnx, gny, gnz), world, rank, args.warmup + args.steps + extra,
-                             args.exchange == "nccl", local)
+        # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
+        # 4 for the 7-point star, 3 or 4 for the box) so K sweeps fuse across the
+        # exchange too (one K-plane exchange per K-sweep round).
+        fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps
+        if world > 1 or loop:
+            spec = dataclasses.replace(spec, halo=max(2, fuse))
+        flags = (_lib.HALO_LO if rank > 0 or loop else 0) | (_lib.HALO_HI if rank < world - 1 or loop else 0)
+        eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
+        if loop:
+            exchanger = LoopbackExchanger() if args.exchange == "loopback" else SelfP2PExchanger(0, 1)
+            info = SlabInfo(0, 3, first, count)  # drives the multi-rank round structure
+        else:
+            exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
+            info = SlabInfo(rank, world, first, count)
+        SlabJacobi.use_signal = not args.no_signal
+        SlabJacobi.use_face_signal = args.face_signal
+        slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
+        slab.init("reference")
+        kernel_id = eng.plan(12)[1]
+        kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
+        if spec.shape == "box" and kname in ("temporal2", "temporalk"):
+            kname = "boxk"  # the box's fused family (kernels_boxk.hip)
+        sweeps_per_launch = eng.fuse_steps if not multi else slab.launches_per_round()
 
-    cells_per_gpu = float(gnx) * gny * count  # this rank's; rank 0 owns the largest slab
-    total_updates = float(gnx) * gny * gnz * args.steps
-    gcell = total_updates / elapsed / 1e9
-    bytes_per_update = 2 * spec.elem_bytes
-    # Roofline of the dominant kernel.  One launch advances its cells by
-    # `sweeps_per_launch` fused sweeps; its compulsory HBM traffic is one read
-    # plus one write of those cells (2 * sizeof(T) per cell, whatever K is):
-    # `achieved` = compulsory bytes / mean launch time, a true fraction of the
-    # HBM peak.  The per-sweep algorithmic figure of SURVEY §8(d) (2 * sizeof(T)
-    # per cell-UPDATE, K per cell per launch) is `effective_GBps`.
-    edge = slab.depth if slab.fused else max(1, slab.depth)
-    # the timed launch: the whole slab (single-GPU job, or face-signalled
-    # slab rounds) or the interior between the two boundary launches
-    whole = not multi or slab.signalled
-    cells_per_launch = cells_per_gpu if whole else cells_per_gpu * (count - 2 * edge) / count
-    compulsory_bytes_launch = cells_per_launch * bytes_per_update
-    alg_bytes_launch = compulsory_bytes_launch * sweeps_per_launch
+        # ---------------- warmup
+        if not multi:
+            # settle the one-time per-shape choice (packed vs equal z-chunks, timed
+            # on the first launch of a shape) outside the timed region whatever W
+            # is: one fused launch a -> b, grid a unchanged
+            eng.prepare()
+            eng.iterate(args.warmup)
+        else:
+            slab.run(args.warmup)
+        barrier()
+
+        # ---------------- timed region: exactly K sweeps
+        stream = torch.cuda.current_stream()
+        t0 = time.perf_counter()
+        if not multi:
+            _, dev_ms = eng.iterate(args.steps, stream=stream, timed=True)
+            kernel_ms_total = dev_ms
+            kernel_launches = eng.plan(args.steps)[0]
+        else:
+            slab.run(args.steps)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.exchange == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            dist.barrier()
+        if multi and slab.signal_timeouts():
+            raise SystemExit("a face-counter wait timed out: the slab rounds did not complete")
+        if multi:
+            # Interior launch time for the roofline, from HIP events on the
+            # interior stream over a few more rounds AFTER the timed region: the
+            # events are extra queue packets (~5 us each per round on MI355X) that
+            # the timed rounds do not carry.
+            slab.start_kernel_timing()
+            extra = max(4, min(args.steps, 8)) * slab.launches_per_round()
+            slab.run(extra)
+            kernel_ms_total, kernel_launches = slab.stop_kernel_timing()
+            if world > 1:
+                dist.barrier()
+        check = None
+        if world > 1 and not args.no_check:
+            check = verify_slabs(eng, slab, spec, (gnx, gny, gnz), world, rank, args.warmup + args.steps + extra,
+                                 args.exchange == "nccl", local)
+        # the timed launch: the whole slab (single-GPU job, or face-signalled
+        # slab rounds) or the interior between the two boundary launches
+        cells_here = float(gnx) * gny * count
+        edge = slab.depth if slab.fused else max(1, slab.depth)
+        whole = not multi or slab.signalled
+        cells_per_launch = cells_here if whole else cells_here * (count - 2 * edge) / count
+        rolling_info = None
+
     if not multi:
         # device time per `sweeps_per_launch` sweeps, charged pro rata (with
         # K = 4 a 1000-step job is 250 fused launches; a K that does not divide
@@ -340,90 +372,214 @@ def main():
         launch_ms = kernel_ms_total * sweeps_per_launch / max(1, args.steps)
     else:
         launch_ms = kernel_ms_total / max(1, kernel_launches)
-    achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9
-    effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
-
+    if rolling:
+        del grid
+        torch.cuda.empty_cache()  # the copy-kernel calibration needs 2 GiB
     if rank == 0:
-        workload = f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{count}"
-        traffic, traffic_entry = load_traffic(workload, kname)
-        desc = pre["desc"].format(n=n)
-        out = {
-            "metric": METRIC,
-            "value": round(gcell, 3),
-            "unit": "Gcell-updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak" if pre["grid"] is None else "strong",
-            "vs_baseline": None,
-            "dtype": "f64" if spec.dtype == "fp64" else "f32",
-            "data": "synthetic: the reference initial condition (x-ghost faces 1, everything else 0)",
-            "config": {
-                "workload": f"{desc} (global {gnx}x{gny}x{gnz}), one step = one sweep",
-                "grid": [gnx, gny, gnz],
-                "kernel": kname,
-                "parallelism": (f"z-slab x{world}" if not loop else
-                                "1 GPU rehearsing an interior rank (periodic halo, two streams, "
-                                + ("device copies)" if args.exchange == "loopback" else "RCCL send/recv to self)")) +
-                               ("" if not multi or loop else
-                                                     ", RCCL halo P2P overlapped" if args.exchange == "nccl"
-                                                     else ", host-staged gloo halo (rehearsal)"),
-                "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
-                "rounds": (None if not multi else
-                           "one face-signalled launch per round" if slab.signalled else
-                           "boundary + interior launches per round"),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": kname,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "bytes_basis": "compulsory: one read + one write of the launch's cells (2 x %d B per cell), "
-                               "%d fused sweeps per launch" % (spec.elem_bytes, sweeps_per_launch),
-                "compulsory_bytes_per_launch": compulsory_bytes_launch,
-                "effective_GBps": round(effective, 1),
-                "effective_basis": "SURVEY 8(d) algorithmic: 2 x %d B per cell-update x %d sweeps per launch"
-                                   % (spec.elem_bytes, sweeps_per_launch),
-                "alg_bytes_per_launch": alg_bytes_launch,
-                "mean_launch_ms": round(launch_ms, 5),
-                "launches": kernel_launches,
-                "launch_timing": ("hipEvents of stencil_iterate over the timed region" if not multi else
-                                  "events around the face-signalled whole-slab launches of extra rounds after the timed region"
-                                  if slab.signalled else
-                                  "events around the interior launches of extra rounds after the timed region"),
-            },
-        }
-        if world > 1:
-            out["multi_gpu_check"] = check if check is not None else {"skipped": "--no-check"}
-        if traffic_entry is not None:
-            out["roofline"]["traffic_source"] = {k: traffic_entry.get(k) for k in
-                                                 ("source", "kernel", "kernel_source_sha", "fresh")}
-        if traffic and launch_ms > 0:
-            # the PMC-measured bytes of one launch (L2->fabric: HBM plus
-            # Infinity-Cache hits) over its live mean duration; traffic well
-            # above the compulsory bytes = re-reads (tile rings, halos)
-            out["roofline"]["traffic_GBps"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
-            out["roofline"]["traffic_frac"] = round(out["roofline"]["traffic_GBps"] / HBM_PEAK_GBPS, 4)
-        try:
-            out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
-        except Exception as exc:  # calibration only
-            out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
-        if world == 1 and not loop and not args.no_cpu_baseline:
-            cb = dict(dtype=spec.dtype, shape=spec.shape)
-            out["cpu_baseline"] = cpu_baseline(min(n, 512), args.cpu_seconds, **cb)
-            # the same loop with OpenMP over the host's cores too
-            out["cpu_baseline_all_cores"] = cpu_baseline(min(n, 512), args.cpu_seconds / 2,
-                                                         threads=host_threads(), **cb)
+        if rolling:
+            parallelism = ("1 GPU, ONE resident grid + a rolling margin of %d planes (stencil_rolling_iterate: "
+                           "%d-plane launches, bitwise the two-grid job)" % (shift, shift - sweeps_per_launch))
+        elif loop:
+            parallelism = ("1 GPU rehearsing an interior rank (periodic halo, two streams, " +
+                           ("device copies)" if args.exchange == "loopback" else "RCCL send/recv to self)"))
         else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+            parallelism = f"z-slab x{world}, one process per GPU (torch.distributed.run)" + (
+                "" if not multi else ", RCCL halo P2P overlapped" if args.exchange == "nccl"
+                else ", host-staged gloo halo (rehearsal)")
+        report(args, pre, spec, kname, (gnx, gny, gnz), world, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
+               kernel_launches, parallelism,
+               rounds=(None if not multi else "one face-signalled launch per round" if slab.signalled else
+                       "boundary + interior launches per round"),
+               launch_timing=("hipEvents of stencil_rolling_iterate over the timed region" if rolling else
+                              "hipEvents of stencil_iterate over the timed region" if not multi else
+                              "events around the face-signalled whole-slab launches of extra rounds after the timed "
+                              "region" if slab.signalled else
+                              "events around the interior launches of extra rounds after the timed region"),
+               workload_key=f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else
+               ("C3_rolling_4096" if rolling else f"{args.config}_slab_{count}"),
+               local=local, check=(check if world > 1 else None), cpu=(world == 1 and not loop),
+               extra_config={"rolling": rolling_info} if rolling else None)
     if world > 1 or args.exchange == "nccl-self":
         dist.destroy_process_group()
+
+
+def slab_job_plan(args, visible: int):
+    """Devices and exchange of the single-process multi-GPU job (no GPU call:
+    `visible` from torch.cuda.device_count()); SystemExit with the reason when
+    it cannot run here."""
+    n = args.gpus
+    if args.exchange not in ("nccl", "copy"):
+        raise SystemExit(f"--exchange {args.exchange} is a torch.distributed rehearsal: without a launcher use "
+                         "nccl (RCCL) or copy (device copies)")
+    if args.share_device:
+        if args.exchange != "copy":
+            raise SystemExit("--share-device without a launcher needs --exchange copy (RCCL refuses two slabs on "
+                             "one GPU)")
+        return [0] * n, "copy"
+    if visible < n:
+        raise SystemExit(f"--gpus {n} needs {n} GPUs, {visible} visible: one process drives them all through the "
+                         "C-ABI slab job (stencil_slab_*); rehearse it on one GPU with --share-device --exchange copy, "
+                         "or launch one process per GPU with torch.distributed.run")
+    return list(range(n)), "rccl" if args.exchange == "nccl" else "copy"
+
+
+def main_slab_job(args):
+    """--gpus N without a launcher: ONE process drives N GPUs through the C-ABI
+    slab job (stencil_slab_create/run/plane_sums, csrc/slab.hip): z-slabs, one
+    per GPU, RCCL send/recv from one host thread, face-signalled rounds -- the
+    shape of the reference's one spawn/join of its whole decomposed job
+    (src/stencil/stencil.cpp:34-53).  Same JSON line as the per-process
+    driver; the roofline from hipEvents on slab 0's compute stream over extra
+    rounds after the timed region; multi_gpu_check against the global grid run
+    as one grid on GPU 0."""
+    import numpy as np
+    import torch
+
+    from stencil_amd.engine import JacobiEngine, SlabJob, StencilSpec
+
+    devices, exchange = slab_job_plan(args, torch.cuda.device_count())
+    n_gpus = args.gpus
+    pre = PRESETS[args.config]
+    n = args.n
+    gnx, gny, gnz = (n, n, n * n_gpus) if pre["grid"] is None else pre["grid"]
+    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
+    job = SlabJob(spec, gnx, gny, gnz, devices, exchange=exchange)
+    job.fill_initial("reference")
+    k = job.info(0)["sweeps_per_round"]
+    # one full round and one shorter remainder round before the timed region:
+    # the one-time costs of both launch paths (schedule trials, first launches)
+    sweeps = k + 1 + args.warmup
+    job.run(k + 1)
+    job.run(args.warmup)
+    elapsed = job.run(args.steps) * 1e-3  # host wall time, every device synchronised at both ends
+    sweeps += args.steps
+    extra = k * max(4, min(args.steps // max(1, k), 8))
+    job.kernel_timing(True)
+    job.run(extra)
+    kt = job.kernel_time()
+    job.kernel_timing(False)
+    sweeps += extra
+    check = None
+    if not args.no_check:
+        got = job.plane_sums()
+        try:
+            need = 2.2 * gnx * gny * gnz * spec.elem_bytes
+            free = torch.cuda.mem_get_info(0)[0]
+            if need > 0.9 * free:
+                check = {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free on GPU 0"}
+            else:
+                ref = JacobiEngine(spec, gnx, gny, gnz, device=0)
+                ref.reset("reference")
+                fin, _ = ref.iterate(sweeps)
+                want = ref.plane_sums(fin)
+                bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
+                check = {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad, "bitwise_equal": bad == 0,
+                         "reference": "the global grid as one grid on GPU 0, same sweeps, per-plane sums"}
+                del ref, fin
+                torch.cuda.empty_cache()
+        except Exception as exc:  # a check, never the measurement
+            check = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    job.close()
+    kname = "boxk" if spec.shape == "box" else "temporalk"
+    where = "GPU 0 shared by every slab (rehearsal)" if args.share_device else f"{n_gpus} GPUs"
+    parallelism = (f"z-slab x{n_gpus}, ONE process driving {where} through the C-ABI slab job (stencil_slab_*), " +
+                   ("RCCL send/recv (ncclCommInitAll)" if exchange == "rccl" else "device-copy halos"))
+    report(args, pre, spec, kname, (gnx, gny, gnz), n_gpus, elapsed, kt["total_ms"] / max(1, kt["launches"]),
+           float(kt["cells_per_launch"]), k, kt["launches"], parallelism,
+           rounds="one face-signalled launch per round" if kt["signalled"] else "boundary + interior launches per round",
+           launch_timing="hipEvents around slab 0's " + ("whole-slab face-signalled" if kt["signalled"] else "interior")
+                         + " launches of extra rounds after the timed region",
+           workload_key=f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz // n_gpus}",
+           local=0, check=check, cpu=False)
+
+
+def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
+           kernel_launches, parallelism, rounds, launch_timing, workload_key, local, check, cpu, extra_config=None):
+    """Print the one JSON line.  Roofline of the dominant kernel: one launch
+    advances its cells by `sweeps_per_launch` fused sweeps; its compulsory HBM
+    traffic is one read plus one write of those cells (2 * sizeof(T) per cell,
+    whatever K is): `achieved` = compulsory bytes / mean launch time, a true
+    fraction of the HBM peak.  The per-sweep algorithmic figure of SURVEY
+    8(d) (2 * sizeof(T) per cell-UPDATE, K per cell per launch) is
+    `effective_GBps`."""
+    from stencil_amd.engine import copy_bandwidth
+    gnx, gny, gnz = grid
+    total_updates = float(gnx) * gny * gnz * args.steps
+    gcell = total_updates / elapsed / 1e9
+    bytes_per_update = 2 * spec.elem_bytes
+    compulsory_bytes_launch = cells_per_launch * bytes_per_update
+    alg_bytes_launch = compulsory_bytes_launch * sweeps_per_launch
+    achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9
+    effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
+    traffic, traffic_entry = load_traffic(workload_key, kname)
+    desc = pre["desc"].format(n=args.n)
+    out = {
+        "metric": METRIC,
+        "value": round(gcell, 3),
+        "unit": "Gcell-updates/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak" if pre["grid"] is None else "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if spec.dtype == "fp64" else "f32",
+        "data": "synthetic: the reference initial condition (x-ghost faces 1, everything else 0)",
+        "config": {
+            "workload": f"{desc} (global {gnx}x{gny}x{gnz}), one step = one sweep",
+            "grid": [gnx, gny, gnz],
+            "kernel": kname,
+            "parallelism": parallelism,
+            "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
+            "rounds": rounds,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kname,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "bytes_basis": "compulsory: one read + one write of the launch's cells (2 x %d B per cell), "
+                           "%d fused sweeps per launch" % (spec.elem_bytes, sweeps_per_launch),
+            "compulsory_bytes_per_launch": compulsory_bytes_launch,
+            "effective_GBps": round(effective, 1),
+            "effective_basis": "SURVEY 8(d) algorithmic: 2 x %d B per cell-update x %d sweeps per launch"
+                               % (spec.elem_bytes, sweeps_per_launch),
+            "alg_bytes_per_launch": alg_bytes_launch,
+            "mean_launch_ms": round(launch_ms, 5),
+            "launches": kernel_launches,
+            "launch_timing": launch_timing,
+        },
+    }
+    if extra_config:
+        out["config"].update(extra_config)
+    if n_gpus > 1:
+        out["multi_gpu_check"] = check if check is not None else {"skipped": "--no-check"}
+    if traffic_entry is not None:
+        out["roofline"]["traffic_source"] = {k: traffic_entry.get(k) for k in
+                                             ("source", "kernel", "kernel_source_sha", "fresh")}
+    if traffic and launch_ms > 0:
+        # the PMC-measured bytes of one launch (L2->fabric: HBM plus
+        # Infinity-Cache hits) over its live mean duration; traffic well
+        # above the compulsory bytes = re-reads (tile rings, halos)
+        out["roofline"]["traffic_GBps"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
+        out["roofline"]["traffic_frac"] = round(out["roofline"]["traffic_GBps"] / HBM_PEAK_GBPS, 4)
+    try:
+        out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
+    except Exception as exc:  # calibration only
+        out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
+    if cpu and not args.no_cpu_baseline:
+        cb = dict(dtype=spec.dtype, shape=spec.shape)
+        n = min(args.n, 512)
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds, **cb)
+        # SURVEY 8d: the same loop with OpenMP over the host's cores too
+        out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads(), **cb)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -55,6 +55,14 @@ extern "C" {
 const char* stencil_strerror(int code);
 const char* stencil_last_error_message(void);
 int stencil_last_error(void);
+/* 0 in libstencil_hip.so (the product: AUTO's plan, the environment knobs
+ * below only); 1 in libstencil_hip_debug.so, which also reads the experiment
+ * knobs (STENCIL_*_CFG workgroup shapes, forced z-chunks and kernel families)
+ * the shape-sweep tests and A/B tools use.  Documented knobs, read by both:
+ * STENCIL_TK_STEPS (3..5) / STENCIL_BOX_STEPS (3, 4) fused sweeps per launch,
+ * STENCIL_TK_PACK / STENCIL_BOXK_PACK (0 equal z-chunks, 1 measured choice,
+ * 2 the model's), STENCIL_SLAB_SIGNAL=0 (slab rounds without face signals). */
+int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */
 
@@ -245,6 +253,28 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
  * launch.  No reference counterpart (the reference has no per-shape state). */
 int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream);
 
+/* One resident grid instead of two (3D, no slab flags): for jobs whose two
+ * ping-pong grids do not fit the GPU -- BASELINE config 3, 4096^3 fp32, is
+ * 2 x 279 GB; one grid plus a few hundred spare planes fits 288 GiB.  The
+ * reference swaps two owner buffers every sweep (src/stencil/stencil.cpp:
+ * 14-21, 88-92; include/stencil/boundary_matrix.hpp:59); here a pass of K
+ * fused sweeps writes plane z of the new grid into the slot D planes below
+ * (down pass) or back (up pass), in launches over z-ranges of D - K planes
+ * ordered so that no launch writes a slot any later read needs.  Results
+ * are bitwise those of stencil_iterate.
+ *   allocation: stencil_rolling_bytes(l, D, &bytes, &K) bytes at `base`;
+ *   the grid at home (position 0) is the layout's grid at base + D*plane*esz,
+ *   shifted (position 1) at base.  Fill / upload the home grid as usual,
+ *   then stencil_rolling_init_margin copies its top ghost plane into the D
+ *   spare slots (the x/y ghost ring must be the same in every plane and the
+ *   z ghost planes alike, as in the reference initial condition).
+ *   stencil_rolling_iterate: `iterations` sweeps from *position (updated);
+ *   launches = kernel launches issued; elapsed_ms as stencil_iterate. */
+int stencil_rolling_bytes(const stencil_layout* l, int64_t shift_planes, int64_t* bytes, int32_t* sweeps_per_pass);
+int stencil_rolling_init_margin(const stencil_layout* l, void* base, int64_t shift_planes, void* stream);
+int stencil_rolling_iterate(const stencil_layout* l, void* base, int64_t shift_planes, uint32_t iterations,
+                            int32_t* position, void* stream, int64_t* launches, float* elapsed_ms);
+
 /* The dispatcher model behind the packed z-chunk schedule, on the host (no
  * GPU needed): `tiles` x-y tiles of `planes` planes on `slots` one-workgroup
  * CU slots, `fill` planes of pipeline fill per chunk (2K for the 7-point
@@ -313,6 +343,15 @@ int stencil_slab_download(stencil_slab_job* job, void* host, int64_t host_row, i
 int stencil_slab_run(stencil_slab_job* job, uint32_t iterations, float* elapsed_ms);
 /* Per-plane interior sums of the current global grid (nz doubles, host). */
 int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
+/* Kernel timing for roofline figures: with timing on, every round records
+ * hipEvents around slab 0's compute launch (the whole slab in face-signalled
+ * rounds, else its interior launch) on that launch's stream.  kernel_time
+ * synchronises and returns the summed device time, the launches timed, the
+ * interior cells one timed launch covers and whether rounds are signalled.
+ * Enabling (or disabling) drops earlier records. */
+int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
+int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,
+                             int32_t* signalled);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,11 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstencil_hip.so")
+# The same kernels linked with the experiment knobs enabled (Makefile,
+# csrc/knobs.cpp): loaded when a STENCIL_* variable other than the documented
+# ones is set, i.e. by the shape-sweep tests and the A/B tools.
+DEBUG_LIB_PATH = os.path.join(_HERE, "libstencil_hip_debug.so")
+API_KNOBS = ("STENCIL_TK_STEPS", "STENCIL_BOX_STEPS", "STENCIL_TK_PACK", "STENCIL_BOXK_PACK", "STENCIL_SLAB_SIGNAL")
 
 STENCIL_OK = 0
 F32, F64 = 0, 1
@@ -28,17 +33,19 @@ KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_Z
 
 # Every symbol include/stencil_hip.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
-    "stencil_strerror", "stencil_last_error_message", "stencil_last_error",
+    "stencil_strerror", "stencil_last_error_message", "stencil_last_error", "stencil_debug_knobs",
     "stencil_iterate_dma", "stencil_iterate_dma_static_unroll", "stencil_iterate_dma_slave_pack",
     "stencil_iterate_rma",
     "stencil_layout_init", "stencil_slow_extent", "stencil_device_count", "stencil_set_device",
     "stencil_synchronize", "stencil_alloc", "stencil_free", "stencil_fill_initial", "stencil_upload",
     "stencil_download", "stencil_copy_planes", "stencil_sweep", "stencil_sweep2", "stencil_sweepk", "stencil_iterate",
-    "stencil_prepare", "stencil_pack_plan", "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth", "stencil_sweepk_geometry", "stencil_sweepk_signal",
+    "stencil_prepare", "stencil_rolling_bytes", "stencil_rolling_init_margin", "stencil_rolling_iterate",
+    "stencil_pack_plan", "stencil_plan", "stencil_plane_sums", "stencil_copy_bandwidth", "stencil_sweepk_geometry", "stencil_sweepk_signal",
     "stencil_wait_counters", "stencil_face_signal_create", "stencil_face_signal_destroy",
     "stencil_face_signal_reset", "stencil_face_signal_read", "stencil_wait_face_signal",
     "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
     "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
+    "stencil_slab_kernel_timing", "stencil_slab_kernel_time",
 )
 
 
@@ -73,24 +80,33 @@ class StencilError(RuntimeError):
         self.code = code
 
 
-_lib = None
+_libs: dict = {}
 
 
-def load() -> ctypes.CDLL:
-    """Load libstencil_hip.so once; raise if it is absent (no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def debug_knobs_requested() -> bool:
+    """Is an experiment knob (a STENCIL_* variable the product ignores) set?"""
+    return any(k.startswith("STENCIL_") and k not in API_KNOBS for k in os.environ)
+
+
+def load(debug: bool | None = None) -> ctypes.CDLL:
+    """Load libstencil_hip.so (or, with experiment knobs set / debug=True, its
+    debug twin) once; raise if it is absent (no fallback)."""
+    if debug is None:
+        debug = debug_knobs_requested()
+    if debug in _libs:
+        return _libs[debug]
+    path = DEBUG_LIB_PATH if debug else LIB_PATH
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: the HIP extension has not been built "
+            f"{path} is missing: the HIP extension has not been built "
             "(run `make` or `python -c 'import __graft_entry__ as g; g.build()'`)")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     P, L = POINTER(Problem), POINTER(Layout)
     sig = {
         "stencil_strerror": (c_char_p, [c_int]),
         "stencil_last_error_message": (c_char_p, []),
         "stencil_last_error": (c_int, []),
+        "stencil_debug_knobs": (c_int, []),
         "stencil_layout_init": (c_int, [P, L]),
         "stencil_slow_extent": (c_int64, [L]),
         "stencil_device_count": (c_int, [POINTER(c_int)]),
@@ -107,6 +123,10 @@ def load() -> ctypes.CDLL:
         "stencil_sweepk": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
         "stencil_iterate": (c_int, [L, c_void_p, c_void_p, c_uint32, c_void_p, POINTER(c_int), POINTER(c_float)]),
         "stencil_prepare": (c_int, [L, c_void_p, c_void_p, c_void_p]),
+        "stencil_rolling_bytes": (c_int, [L, c_int64, POINTER(c_int64), POINTER(c_int32)]),
+        "stencil_rolling_init_margin": (c_int, [L, c_void_p, c_int64, c_void_p]),
+        "stencil_rolling_iterate": (c_int, [L, c_void_p, c_int64, c_uint32, POINTER(c_int32), c_void_p,
+                                            POINTER(c_int64), POINTER(c_float)]),
         "stencil_pack_plan": (c_int, [c_int64, c_int64, c_int32, c_int32, c_int32, POINTER(c_int64),
                                       POINTER(c_int64), POINTER(c_int64)]),
         "stencil_plan": (c_int, [L, c_uint32, POINTER(c_int64), POINTER(c_int32)]),
@@ -132,6 +152,9 @@ def load() -> ctypes.CDLL:
         "stencil_slab_download": (c_int, [c_void_p, c_void_p, c_int64, c_int64]),
         "stencil_slab_run": (c_int, [c_void_p, c_uint32, POINTER(c_float)]),
         "stencil_slab_plane_sums": (c_int, [c_void_p, POINTER(c_double)]),
+        "stencil_slab_kernel_timing": (c_int, [c_void_p, c_int32]),
+        "stencil_slab_kernel_time": (c_int, [c_void_p, POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
+                                             POINTER(c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -142,13 +165,15 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = None
         fn.argtypes = [POINTER(Arguments)]
-    _lib = lib
+    _libs[debug] = lib
     return lib
 
 
-def check(rc: int, where: str) -> None:
+def check(rc: int, where: str, lib: ctypes.CDLL | None = None) -> None:
+    """Raise StencilError for a failed call; `lib` = the library that made it
+    (its per-thread error message)."""
     if rc != STENCIL_OK:
-        lib = load()
+        lib = lib or load()
         msg = (lib.stencil_last_error_message() or b"").decode(errors="replace")
         raise StencilError(rc, where, msg or lib.stencil_strerror(rc).decode())
 

@@ -116,8 +116,7 @@ bool iterate_fused(const stencil_problem& p) {
     // (the 2-step BOXK kernel: +50-90 % fp64, +9-37 % fp32 over the single
     // sweep on MI355X).
     if (p.kernel != STENCIL_KERNEL_AUTO || !fused_supported(p)) return false;
-    const char* e = std::getenv("STENCIL_NO_T2");
-    return !(e && *e && *e != '0');
+    return knob("STENCIL_NO_T2", 0) == 0;
 }
 
 // Steps per launch of the deep temporal-blocking family (kernels_strip.hip,
@@ -131,13 +130,11 @@ int iterate_tk_steps(const stencil_problem& p) {
     if (!temporal2_supports(p)) return 0;
     if (p.kernel == STENCIL_KERNEL_AUTO) {
         if (!iterate_fused(p)) return 0;
-        const char* e = std::getenv("STENCIL_NO_TK");
-        if (e && *e && *e != '0') return 0;
+        if (knob("STENCIL_NO_TK", 0) != 0) return 0;
     } else if (p.kernel != STENCIL_KERNEL_TEMPORALK) {
         return 0;
     }
-    const char* k = std::getenv("STENCIL_TK_STEPS");
-    const int steps = k && *k ? std::atoi(k) : (p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4);
+    const int steps = api_knob("STENCIL_TK_STEPS", p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4);
     return steps >= 3 && steps <= 5 ? steps : 0;
 }
 
@@ -153,8 +150,7 @@ int iterate_tk_steps(const stencil_problem& p) {
 int iterate_box_steps(const stencil_problem& p) {
     if (!box27_supports(p)) return 0;
     if (!(p.kernel == STENCIL_KERNEL_TEMPORALK || (p.kernel == STENCIL_KERNEL_AUTO && iterate_fused(p)))) return 0;
-    const char* k = std::getenv("STENCIL_BOX_STEPS");
-    const int steps = k && *k ? std::atoi(k) : (p.dtype == STENCIL_F64 && p.nx * p.ny >= int64_t(640) * 640 ? 4 : 3);
+    const int steps = api_knob("STENCIL_BOX_STEPS", p.dtype == STENCIL_F64 && p.nx * p.ny >= int64_t(640) * 640 ? 4 : 3);
     return steps == 3 || steps == 4 ? steps : 0;
 }
 
@@ -163,8 +159,7 @@ int iterate_box_steps(const stencil_problem& p) {
 bool iterate_tb2d(const stencil_problem& p) {
     if (!tb2d_supports(p)) return false;
     if (p.kernel == STENCIL_KERNEL_TEMPORAL2 || p.kernel == STENCIL_KERNEL_PERSISTENT) return true;
-    const char* e = std::getenv("STENCIL_NO_T2");
-    return p.kernel == STENCIL_KERNEL_AUTO && !(e && *e && *e != '0');
+    return p.kernel == STENCIL_KERNEL_AUTO && knob("STENCIL_NO_T2", 0) == 0;
 }
 
 // The whole 2D job as one persistent launch (kernels_tb2dp.hip): explicit
@@ -173,8 +168,7 @@ bool iterate_tb2d(const stencil_problem& p) {
 bool iterate_persistent(const stencil_problem& p) {
     if (!tb2dp_supports(p)) return false;
     if (p.kernel == STENCIL_KERNEL_PERSISTENT) return true;
-    const char* e = std::getenv("STENCIL_TB2DP");
-    return p.kernel == STENCIL_KERNEL_AUTO && iterate_tb2d(p) && e && *e == '1';
+    return p.kernel == STENCIL_KERNEL_AUTO && iterate_tb2d(p) && knob("STENCIL_TB2DP", 0) == 1;
 }
 
 int launch_single(const stencil_layout& l, const void* in, void* out, int64_t b, int64_t e, hipStream_t s) {
@@ -501,8 +495,7 @@ int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end,
         return set_error(STENCIL_EUNSUPPORTED, "geometry: the K-step kernel of the 3D r=1 7-point star, steps 3..5");
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
-    const char* strip = std::getenv("STENCIL_TK_STRIP");
-    if (strip && *strip && std::atoi(strip) == 0)  // the interleaved-row kernel has no dry mode
+    if (knob("STENCIL_TK_STRIP", 1) == 0)  // the interleaved-row kernel has no dry mode
         return set_error(STENCIL_EUNSUPPORTED, "geometry: not the strip kernel (STENCIL_TK_STRIP=0)");
     LaunchInfo info;
     tl_dry_launch = &info;
@@ -714,6 +707,125 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
     }
     if (rc != STENCIL_OK) return rc;
     if (final_in_b) *final_in_b = in == b ? 1 : 0;
+    if (elapsed_ms) {
+        STENCIL_HIP_CHECK(hipEventRecord(e1, s));
+        STENCIL_HIP_CHECK(hipEventSynchronize(e1));
+        STENCIL_HIP_CHECK(hipEventElapsedTime(elapsed_ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    clear_error();
+    return STENCIL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// One resident grid (include/stencil_hip.h part 2b).  The reference keeps two
+// owner buffers and swaps them every sweep (stencil.cpp:14-21, 88-92;
+// boundary_matrix.hpp:59): at BASELINE config 3 (4096^3 fp32) that is 2 x 279
+// GB, more than one MI355X holds.  Here one grid plus D spare planes below it:
+// a pass of k fused sweeps writes plane z of the new grid into slot z - D
+// (down pass) or, from there, back into slot z (up pass), as ceil(nz / S)
+// launches over z-ranges of S = D - K planes (K = the deepest pass), taken
+// bottom-up on the down pass and top-down on the up pass.  A launch over
+// [jS, jS + S) reads slots [jS - k, jS + S + k) and writes slots
+// [jS - D, jS + S - D) (down): disjoint, and no later launch reads what it
+// writes; the up pass mirrors it.  Same kernels, same arithmetic: bitwise
+// the two-grid job.  Slots are indexed from the home grid's interior plane 0:
+// the allocation holds slots [-D - zg, nz + zg), home = slot -zg.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace stencil {
+namespace {
+
+int rolling_steps(const stencil_problem& p) {
+    if (const int k = iterate_tk_steps(p)) return k;
+    if (const int k = iterate_box_steps(p)) return k;
+    return iterate_fused(p) ? 2 : 1;
+}
+
+int check_rolling(const stencil_layout* l, int64_t shift) {
+    if (int rc = check_layout(l)) return rc;
+    const stencil_problem& p = l->prob;
+    if (p.dims != 3) return set_error(STENCIL_EUNSUPPORTED, "rolling jobs cover 3D grids (z passes)");
+    if (p.flags != 0) return set_error(STENCIL_EINVAL, "rolling jobs take no slab halo flags");
+    const int k = rolling_steps(p);
+    if (shift < k + 1) return set_error(STENCIL_EINVAL, "shift must be at least %d planes (got %lld)", k + 1, (long long)shift);
+    return STENCIL_OK;
+}
+
+}  // namespace
+}  // namespace stencil
+
+extern "C" {
+
+int stencil_rolling_bytes(const stencil_layout* l, int64_t shift_planes, int64_t* bytes, int32_t* sweeps_per_pass) {
+    if (int rc = check_rolling(l, shift_planes)) return rc;
+    if (bytes) *bytes = (l->planes + shift_planes) * l->plane * int64_t(elem_size(l->prob)) + 256;
+    if (sweeps_per_pass) *sweeps_per_pass = rolling_steps(l->prob);
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_rolling_init_margin(const stencil_layout* l, void* base, int64_t shift_planes, void* stream) {
+    if (int rc = check_rolling(l, shift_planes)) return rc;
+    if (!base) return set_error(STENCIL_EINVAL, "null grid");
+    const size_t pe = size_t(l->plane) * elem_size(l->prob);
+    char* home = static_cast<char*>(base) + size_t(shift_planes) * pe;
+    const char* ghost = home + size_t(l->zghost + l->prob.nz) * pe;  // the home grid's top ghost plane
+    for (int64_t i = 0; i < shift_planes; ++i)
+        STENCIL_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(base) + size_t(i) * pe, ghost, pe, hipMemcpyDeviceToDevice,
+                                         as_stream(stream)));
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_rolling_iterate(const stencil_layout* l, void* base, int64_t shift_planes, uint32_t iterations,
+                            int32_t* position, void* stream, int64_t* launches, float* elapsed_ms) {
+    if (int rc = check_rolling(l, shift_planes)) return rc;
+    if (!base || !position || (*position != 0 && *position != 1))
+        return set_error(STENCIL_EINVAL, "null grid or position not 0 (home) / 1 (shifted)");
+    hipStream_t s = as_stream(stream);
+    const stencil_problem& p = l->prob;
+    const int64_t nz = p.nz, zg = l->zghost, D = shift_planes;
+    const int K = rolling_steps(p);
+    const int64_t S = D - K;
+    const size_t pe = size_t(l->plane) * elem_size(p);
+    char* shifted = static_cast<char*>(base);
+    char* home = shifted + size_t(D) * pe;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (elapsed_ms) {
+        STENCIL_HIP_CHECK(hipEventCreate(&e0));
+        STENCIL_HIP_CHECK(hipEventCreate(&e1));
+        STENCIL_HIP_CHECK(hipEventRecord(e0, s));
+    }
+    int64_t n = 0;
+    const int64_t J = nz > 0 ? (nz + S - 1) / S : 0;
+    for (uint32_t done = 0; done < iterations;) {
+        int k = int(std::min<uint32_t>(uint32_t(K), iterations - done));
+        if (k == 2 && !fused_supported(p)) k = 1;
+        const bool down = *position == 0;
+        for (int64_t i = 0; i < J; ++i) {
+            const int64_t j = down ? i : J - 1 - i;
+            const int64_t b = j * S, e = std::min(nz, b + S);
+            const int rc = down ? stencil_sweepk(l, home, shifted, b, e, k, stream)
+                                : stencil_sweepk(l, shifted, home, b, e, k, stream);
+            if (rc != STENCIL_OK) return rc;
+            ++n;
+        }
+        // the slots the pass overwrote that are ghost planes of the grid it
+        // produced: the shifted grid's top ghosts (from the home grid's,
+        // never written) / the home grid's bottom ghosts (from the shifted
+        // grid's, never written)
+        if (down)
+            STENCIL_HIP_CHECK(hipMemcpyAsync(shifted + size_t(zg + nz) * pe, home + size_t(zg + nz) * pe, size_t(zg) * pe,
+                                             hipMemcpyDeviceToDevice, s));
+        else
+            STENCIL_HIP_CHECK(hipMemcpyAsync(home, shifted, size_t(zg) * pe, hipMemcpyDeviceToDevice, s));
+        *position = down ? 1 : 0;
+        done += uint32_t(k);
+    }
+    if (launches) *launches = n;
     if (elapsed_ms) {
         STENCIL_HIP_CHECK(hipEventRecord(e1, s));
         STENCIL_HIP_CHECK(hipEventSynchronize(e1));

@@ -77,7 +77,7 @@ inline T avg_weight(const stencil_problem& p) {
 struct LaunchInfo {
     int64_t workgroups = 0;
     int zchunk = 0;   // planes per z-chunk; 0 = one balanced share per workgroup
-    int packed = 0;   // the packed longest-first schedule is used
+    int packed = 0;   // 0 equal chunks, 1 packed (measured faster), 2 packed by the model, not yet measured
     int steps = 0;
 };
 extern thread_local LaunchInfo* tl_dry_launch;
@@ -87,13 +87,18 @@ extern thread_local LaunchInfo* tl_dry_launch;
 // longest first, Lc chosen by simulating the dispatcher with `fill` steps of
 // pipeline fill per chunk; a device table of {tile, first plane, planes} per
 // workgroup when it beats equal chunks of zc planes, else *sched untouched.
-// `family` keeps the caches of different kernels apart.  *verdict (when
-// asked for) points at the shape's measured choice: kPackUntested until
-// pick_schedule has timed both grids on this device, then kPackPacked or
-// kPackEqual.
+// The cache is keyed by the kernel itself (one instantiation: dtype and shape)
+// and the device.  *verdict (when asked for) points at the shape's measured
+// choice: kPackUntested until pick_schedule has timed both grids on this
+// device, then kPackPacked or kPackEqual.  The table is searched on the host
+// and uploaded on the first real launch on `s` (stream-ordered, one host
+// wait); `dry` (stencil_sweepk_geometry) and launches into a capturing stream
+// upload nothing -- a capturing launch runs equal chunks -- and a dry call
+// reports a table that would be used through *sched = kDrySchedule.
 enum { kPackUntested = 0, kPackPacked = 1, kPackEqual = 2 };
-int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr);
+extern const int* const kDrySchedule;
+int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
+                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr);
 
 // The dispatcher model behind packed_schedule mispredicts some shapes badly
 // (measured: 504 x 512 x 512 fp64 packed 0.555 vs equal 0.450 ms per launch,
@@ -107,6 +112,17 @@ int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int f
 int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<hipError_t(bool)>& launch);
 // STENCIL_TK_PACK / STENCIL_BOXK_PACK: 0 = equal chunks, 1 = measured choice
 // (default), 2 = the model's choice without measuring
+
+// Environment knobs.  api_knob: the few include/stencil_hip.h documents
+// (STENCIL_TK_STEPS, STENCIL_BOX_STEPS, STENCIL_TK_PACK, STENCIL_BOXK_PACK,
+// STENCIL_SLAB_SIGNAL), read in every build.  knob: the experiment selectors
+// (workgroup shapes, forced z-chunks and kernel families, diagnostics) -- read
+// only by the debug library (knobs.cpp built with -DSTENCIL_DEBUG_KNOBS into
+// stencil_amd/libstencil_hip_debug.so, which the shape-sweep tests load); in
+// the product library knob() returns `dflt`, so it runs AUTO's plan and
+// nothing else.
+int knob(const char* name, int dflt);
+int api_knob(const char* name, int dflt);
 
 // ---- kernel entry points (defined in kernels_*.hip) ----------------------
 int launch_direct(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

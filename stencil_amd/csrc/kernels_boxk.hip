@@ -592,10 +592,7 @@ __global__ void __launch_bounds__(64 * NW)
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s && *s ? std::atoi(s) : dflt;
-}
+int env_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, bool SIG = false, bool STRIP = false>
 int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
@@ -668,11 +665,13 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const int* sched = nullptr;
     std::atomic<int>* verdict = nullptr;
     const int64_t nb_equal = nb;
-    const int pack_mode = env_int("STENCIL_BOXK_PACK", sizeof(T) == 8 ? 1 : 0);
+    const int pack_mode = api_knob("STENCIL_BOXK_PACK", sizeof(T) == 8 ? 1 : 0);
     if (STRIP && !SIG && slots > 0 && pack_mode && !(lo || hi)) {
         int dev = 0;
         STENCIL_HIP_CHECK(hipGetDevice(&dev));
-        if (const int rc = packed_schedule(1, dev, tiles, nz, K, 3 * K, slots, zc, &sched, &nb, &verdict)) return rc;
+        if (const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, tiles, nz, K, 3 * K, slots, zc, s,
+                                           false, &sched, &nb, &verdict))
+            return rc;
         if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }

@@ -410,10 +410,7 @@ __global__ void __launch_bounds__(64 * NW)
     }
 }
 
-int senv_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s && *s ? std::atoi(s) : dflt;
-}
+int senv_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
           bool FP = true>
@@ -492,10 +489,11 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     // gain AND the first launch measured it faster (pick_schedule; 512^3 fp64
     // 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a multi-GPU
     // job, whose one-round grid above is deliberate
-    const int pack_mode = senv_int("STENCIL_TK_PACK", 1);
+    const int pack_mode = api_knob("STENCIL_TK_PACK", 1);
     if (!SIG && zc > 0 && pack_mode && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
         !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
-        const int rc = packed_schedule(0, dev, gx * gy, nz, K, 2 * K, slots, zc, &sched, &nb, &verdict);
+        const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, slots, zc, s,
+                                       tl_dry_launch != nullptr, &sched, &nb, &verdict);
         if (rc != STENCIL_OK) return rc;
         if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
@@ -520,7 +518,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if (LaunchInfo* info = tl_dry_launch) {  // stencil_sweepk_geometry: describe, do not launch
         info->workgroups = nb;
         info->zchunk = zc;
-        info->packed = sched != nullptr;
+        info->packed = sched == nullptr ? 0 : (verdict && verdict->load() == kPackUntested ? 2 : 1);
         info->steps = K;
         return STENCIL_OK;
     }
@@ -599,6 +597,8 @@ static void pack_search(int64_t tiles, int64_t nz, int fill, int slots, int zc, 
     *best_out = best;
 }
 
+const int* const kDrySchedule = reinterpret_cast<const int*>(uintptr_t(16));
+
 // STENCIL_TK_PACK (default 1; 0 = equal chunks): chunks of Lc planes per tile (the last one
 // shorter), longest first -- every tile's full chunks start in z lock-step,
 // the short remainders fill the CUs the full chunks leave idle.  Lc is the
@@ -606,56 +606,73 @@ static void pack_search(int64_t tiles, int64_t nz, int fill, int slots, int zc, 
 // equal-chunk grid (zc planes per chunk) by 2 %.  The table is built once per
 // shape and kept for the process.
 // The table lives in the memory of the device it was built on: the cache is
-// keyed by device ordinal and guarded (a process may drive several GPUs from
-// several threads: stencil_set_device is per thread).
-int packed_schedule(int family, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    const int** sched, int64_t* nb, std::atomic<int>** verdict) {
+// keyed by kernel and device ordinal and guarded (a process may drive several
+// GPUs from several threads: stencil_set_device is per thread).
+int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
+                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict) {
     // Only grids of few tiles: with more than 2 tiles per slot the equal
     // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
     // Gcell/s), and the search would cost host time at the first launch.
     if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
     if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
     struct Entry {
-        int* table = nullptr;
+        std::vector<int> host;  // {tile, first plane, planes} per workgroup; empty: not used
+        int* table = nullptr;   // its device copy, uploaded on the first real launch
         int64_t workgroups = 0;
         std::atomic<int> verdict{kPackUntested};
     };
     static std::mutex mu;
     // map nodes never move: the verdict's address stays valid for the process
-    static std::map<std::tuple<int, int, int64_t, int64_t, int, int, int>, Entry> cache;
+    static std::map<std::tuple<const void*, int, int64_t, int64_t, int, int, int>, Entry> cache;
     std::lock_guard<std::mutex> lock(mu);
     // STENCIL_TK_PACK_LC (experiments): chunks of exactly this many planes,
     // used whatever the model says
     const int force_lc = senv_int("STENCIL_TK_PACK_LC", 0);
-    const auto key = std::make_tuple(family, dev, tiles, nz, K, slots, force_lc);
+    const auto key = std::make_tuple(kern, dev, tiles, nz, K, slots, force_lc);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
         std::vector<int> best_tab;
         int64_t base = 0, best = 0;
         pack_search(tiles, nz, fill, slots, zc, force_lc, &best_tab, &base, &best);
-        int* d = nullptr;
-        int64_t n = 0;
-        if (!best_tab.empty() && best * 50 < base * 49) {
-            if (hipMalloc(&d, best_tab.size() * sizeof(int)) != hipSuccess ||
-                hipMemcpy(d, best_tab.data(), best_tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-                // a pageable H2D copy may return before its DMA lands, and the
-                // launch goes to another stream: wait for it (once per shape)
-                hipDeviceSynchronize() != hipSuccess)
-                return set_error(STENCIL_EHIP, "packed schedule upload failed");
-            n = int64_t(best_tab.size() / 3);
+        hit = cache.try_emplace(key).first;
+        if (!best_tab.empty() && (best * 50 < base * 49 || force_lc > 0)) {
+            hit->second.workgroups = int64_t(best_tab.size() / 3);
+            hit->second.host = std::move(best_tab);
         }
         if (senv_int("STENCIL_TK_VERBOSE", 0))
-            std::fprintf(stderr, "pack (family %d): equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n", family,
-                         (long long)base, (long long)best, (long long)n, d ? "" : " -- not used");
-        hit = cache.try_emplace(key).first;
-        hit->second.table = d;
-        hit->second.workgroups = n;
+            std::fprintf(stderr, "pack: equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n",
+                         (long long)base, (long long)best, (long long)hit->second.workgroups,
+                         hit->second.host.empty() ? " -- not used" : "");
     }
-    if (hit->second.table) {
-        *sched = hit->second.table;
-        *nb = hit->second.workgroups;
-        if (verdict) *verdict = &hit->second.verdict;
+    Entry& e = hit->second;
+    if (e.host.empty()) return STENCIL_OK;
+    if (dry) {  // geometry query: no upload, no GPU work
+        *sched = kDrySchedule;
+        *nb = e.workgroups;
+        if (verdict) *verdict = &e.verdict;
+        return STENCIL_OK;
     }
+    if (!e.table) {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+            (void)hipGetLastError();
+            cap = hipStreamCaptureStatusActive;
+        }
+        if (cap != hipStreamCaptureStatusNone) return STENCIL_OK;  // no allocation inside a capture: equal chunks
+        int* d = nullptr;
+        if (hipMalloc(&d, e.host.size() * sizeof(int)) != hipSuccess ||
+            hipMemcpyAsync(d, e.host.data(), e.host.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess ||
+            // ordered before this launch on `s`; the wait (once per shape) also
+            // orders it before launches the caller puts on other streams
+            hipStreamSynchronize(s) != hipSuccess) {
+            if (d) (void)hipFree(d);
+            return set_error(STENCIL_EHIP, "packed schedule upload failed");
+        }
+        e.table = d;
+    }
+    *sched = e.table;
+    *nb = e.workgroups;
+    if (verdict) *verdict = &e.verdict;
     return STENCIL_OK;
 }
 

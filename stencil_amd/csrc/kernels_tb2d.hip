@@ -252,10 +252,7 @@ int launch_tbs(const stencil_layout& l, const void* in, void* out, int steps, hi
     return STENCIL_OK;
 }
 
-int tenv_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e && *e ? std::atoi(e) : dflt;
-}
+int tenv_int(const char* name, int dflt) { return knob(name, dflt); }
 
 // region shapes (STENCIL_TB2D_CFG = waves * 1000 + region height)
 template <typename T, int ORDER, int R>
@@ -312,9 +309,9 @@ bool tb2d_supports(const stencil_problem& p) {
 }
 
 int tb2d_max_steps(const stencil_problem& p) {
-    const char* e = std::getenv("STENCIL_TB2D_K");
-    const bool forced = e && *e;
-    const int k = forced ? std::atoi(e) : 8;
+    const int kf = knob("STENCIL_TB2D_K", 0);
+    const bool forced = kf != 0;
+    const int k = forced ? kf : 8;
     // default: keep the output tile at least half of a 32-row region; an
     // explicit K may go up to a 16-cell-wide tile of the 64-wide region
     const int cap = std::max(1, (forced ? 24 : 8) / p.radius);
@@ -341,9 +338,8 @@ int strip_slots() {
 int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
     const stencil_problem& p = l.prob;
     const int base = tb2d_max_steps(p);
-    const char* e = std::getenv("STENCIL_TB2D_K");
     const int cfg = tenv_int("STENCIL_TB2D_CFG", 0);
-    if ((e && *e) || p.radius > 2 || (cfg != 0 && cfg != 92808 && cfg != 92416)) return base;  // 128 x 64 only
+    if (knob("STENCIL_TB2D_K", 0) != 0 || p.radius > 2 || (cfg != 0 && cfg != 92808 && cfg != 92416)) return base;  // 128 x 64 only
     const int slots = strip_slots();
     (void)hipGetLastError();
     if (slots <= 0) return base;
@@ -366,8 +362,7 @@ int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
 bool tb2d1_fits(const stencil_layout& l) {
     const stencil_problem& p = l.prob;
     if (!tb2d_supports(p) || p.nx <= 0 || p.ny <= 0) return false;
-    const char* e = std::getenv("STENCIL_TB2D_SINGLE");
-    if (e && *e == '0') return false;
+    if (knob("STENCIL_TB2D_SINGLE", 1) == 0) return false;
     const int64_t esz = p.dtype == STENCIL_F32 ? 4 : 8;
     const int64_t lds = 2 * (p.nx + 2 * p.radius) * (p.ny + 2 * p.radius) * esz;
     return p.nx * p.ny <= int64_t(k1Threads) * k1MaxCells && lds <= 160 * 1024;

@@ -113,7 +113,7 @@ int launch_tbp(const stencil_layout& l, void* a, void* b, uint32_t iterations, i
     const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
 #ifdef STENCIL_DIAG
     // timing experiments only (results wrong on purpose): never in the product build
-    static const int diag = [] { const char* e = std::getenv("STENCIL_TB2DP_DIAG"); return e ? std::atoi(e) : 0; }();
+    static const int diag = knob("STENCIL_TB2DP_DIAG", 0);
     auto kern = diag == 1 ? tb2dp<T, ORDER, R, V, RY, NW, 1> : diag == 2 ? tb2dp<T, ORDER, R, V, RY, NW, 2>
                                                                          : tb2dp<T, ORDER, R, V, RY, NW, 0>;
 #else
@@ -166,8 +166,7 @@ bool tb2dp_supports(const stencil_problem& p) {
 }
 
 int tb2dp_steps(const stencil_problem& p) {
-    const char* e = std::getenv("STENCIL_TB2DP_K");
-    const int k = e && *e ? std::atoi(e) : 8 / p.radius;
+    const int k = knob("STENCIL_TB2DP_K", 8 / p.radius);
     return std::max(1, std::min(k, 24 / p.radius));
 }
 

@@ -429,10 +429,7 @@ __global__ void __launch_bounds__(64 * NW)
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s && *s ? std::atoi(s) : dflt;
-}
+int env_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int R = 4, bool LC = false>
 int launch_t2(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

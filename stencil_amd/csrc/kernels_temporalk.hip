@@ -277,10 +277,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WP
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s && *s ? std::atoi(s) : dflt;
-}
+int env_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, int R, bool DPPX = false, bool AL = false, int XRO = 0,
           int WPE = 1, bool SB = false>

@@ -198,10 +198,7 @@ __global__ void __launch_bounds__(64 * kBY)
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* s = std::getenv(name);
-    return s && *s ? std::atoi(s) : dflt;
-}
+int env_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY>
 int launch_zm(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,

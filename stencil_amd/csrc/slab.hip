@@ -8,7 +8,7 @@
 // Here the blocks are contiguous z-slabs of the global grid, one per GPU
 // (remainder planes to the lowest slabs), each with K ghost planes per shared
 // face, where K is the number of sweeps stencil_iterate fuses into one launch
-// for the problem (7-point star: 4 or 5; box: 2): one round = K fused sweeps
+// for the problem (7-point star: 4 or 5; box: 3 or 4): one round = K fused sweeps
 // + one exchange of K whole planes with each neighbour (temporal blocking
 // across GPUs; the halo planes are advanced on chip).  Per slab and round:
 //   stream A (high priority): the K boundary planes of each face, then the
@@ -108,6 +108,11 @@ struct stencil_slab_job {
     bool chained = false;  // round events recorded since the last join
     bool signal = false;   // full rounds as face-signalled single launches
     std::vector<stencil::Slab> s;
+    // stencil_slab_kernel_timing: hipEvents around slab 0's compute launch of
+    // every round (the whole slab in face-signalled rounds, else the interior)
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    int64_t timed_cells = 0;
 };
 
 namespace stencil {
@@ -116,6 +121,32 @@ namespace {
 int set_dev(int d) {
     STENCIL_HIP_CHECK(hipSetDevice(d));
     return STENCIL_OK;
+}
+
+// Timing events around slab 0's compute launch (the caller has set slab 0's
+// device): begin() before it, end() after it, on the launch's stream.
+int time_begin(stencil_slab_job& j, size_t slab, hipStream_t st) {
+    if (!j.timing || slab != 0) return STENCIL_OK;
+    hipEvent_t a = nullptr, b = nullptr;
+    STENCIL_HIP_CHECK(hipEventCreate(&a));
+    STENCIL_HIP_CHECK(hipEventCreate(&b));
+    j.tev.emplace_back(a, b);
+    STENCIL_HIP_CHECK(hipEventRecord(a, st));
+    return STENCIL_OK;
+}
+int time_end(stencil_slab_job& j, size_t slab, hipStream_t st, int64_t cells) {
+    if (!j.timing || slab != 0) return STENCIL_OK;
+    STENCIL_HIP_CHECK(hipEventRecord(j.tev.back().second, st));
+    j.timed_cells = cells;
+    return STENCIL_OK;
+}
+void drop_timing(stencil_slab_job& j) {
+    for (auto& e : j.tev) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    j.tev.clear();
+    j.timed_cells = 0;
 }
 
 // Sweeps stencil_iterate fuses into one launch for `p` (its plan over a
@@ -223,7 +254,8 @@ int sync_all(stencil_slab_job& j) {
 int slab_round(stencil_slab_job& j, int k) {
     const bool src_a = j.cur_is_a;
     const int64_t edge = j.depth;
-    for (Slab& s : j.s) {
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab& s = j.s[i];
         if (int rc = set_dev(s.device)) return rc;
         void* src = src_a ? s.a : s.b;
         void* dst = src_a ? s.b : s.a;
@@ -233,13 +265,18 @@ int slab_round(stencil_slab_job& j, int k) {
             STENCIL_HIP_CHECK(hipStreamWaitEvent(s.sb, s.ev_bnd, 0));
             STENCIL_HIP_CHECK(hipStreamWaitEvent(s.sa, s.ev_int, 0));
         }
+        const int64_t plane_cells = s.l.prob.nx * s.l.prob.ny;
         if (s.n > 2 * edge) {
+            if (int rc = time_begin(j, i, s.sb)) return rc;
             if (int rc = stencil_sweepk(&s.l, src, dst, edge, s.n - edge, k, s.sb)) return rc;
+            if (int rc = time_end(j, i, s.sb, plane_cells * (s.n - 2 * edge))) return rc;
             STENCIL_HIP_CHECK(hipEventRecord(s.ev_int, s.sb));
             if (int rc = stencil_sweepk(&s.l, src, dst, 0, edge, k, s.sa)) return rc;
             if (int rc = stencil_sweepk(&s.l, src, dst, s.n - edge, s.n, k, s.sa)) return rc;
         } else {
+            if (int rc = time_begin(j, i, s.sa)) return rc;
             if (int rc = stencil_sweepk(&s.l, src, dst, 0, s.n, k, s.sa)) return rc;
+            if (int rc = time_end(j, i, s.sa, plane_cells * s.n)) return rc;
             STENCIL_HIP_CHECK(hipEventRecord(s.ev_int, s.sa));
         }
         if (j.exchange == STENCIL_EXCHANGE_COPY)  // the face copies read whole rounds
@@ -267,13 +304,16 @@ int slab_round(stencil_slab_job& j, int k) {
 // after launch(r-1) ended (one stream).
 int slab_round_signal(stencil_slab_job& j, int k) {
     const bool src_a = j.cur_is_a;
-    for (Slab& s : j.s) {
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab& s = j.s[i];
         if (int rc = set_dev(s.device)) return rc;
         void* src = src_a ? s.a : s.b;
         void* dst = src_a ? s.b : s.a;
         if (j.chained) STENCIL_HIP_CHECK(hipStreamWaitEvent(s.sb, s.ev_bnd, 0));
         int nsig = 0;
+        if (int rc = time_begin(j, i, s.sb)) return rc;
         if (int rc = stencil_sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, nullptr, &nsig, s.sb)) return rc;
+        if (int rc = time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n)) return rc;
         STENCIL_HIP_CHECK(hipEventRecord(s.ev_int, s.sb));
         s.sig_target += uint32_t(nsig);
         if (int rc = stencil_wait_counters(s.counters, s.sig_target, s.sig_target, s.counters + 2, s.sa)) return rc;
@@ -305,6 +345,10 @@ int check_signal_timeouts(stencil_slab_job& j) {
 
 void release(stencil_slab_job* j) {
     if (!j) return;
+    if (!j->s.empty()) {
+        (void)hipSetDevice(j->s[0].device);
+        drop_timing(*j);
+    }
     for (Slab& s : j->s) {
         (void)hipSetDevice(s.device);
         if (s.sa) (void)hipStreamSynchronize(s.sa);
@@ -361,7 +405,7 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
     // 7-point star K = 3..5, box K = 2..4); STENCIL_SLAB_SIGNAL=0: boundary +
     // interior launches
     {
-        const char* e = std::getenv("STENCIL_SLAB_SIGNAL");
+        const bool off = api_knob("STENCIL_SLAB_SIGNAL", 1) == 0;
         const bool star = g.shape == STENCIL_STAR && j->k >= 3 && j->k <= 5;
         const bool box = g.shape == STENCIL_BOX && j->k >= 2 && j->k <= 4;
         // and only with one slab per GPU: slabs sharing a GPU multiplex their
@@ -371,7 +415,7 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
         for (int i = 0; i < ngpus; ++i)
             for (int k = 0; k < i; ++k) distinct = distinct && devs[size_t(i)] != devs[size_t(k)];
         j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct &&
-                    !(e && *e == '0');
+                    !off;
     }
     const int64_t base = g.nz / ngpus, rem = g.nz % ngpus;
     j->s.resize(size_t(ngpus));
@@ -457,8 +501,11 @@ int stencil_slab_fill_initial(stencil_slab_job* job, int32_t init_kind, uint64_t
 
 int stencil_slab_upload(stencil_slab_job* job, const void* host, int64_t host_row, int64_t host_rows) {
     if (!job || !host) return set_error(STENCIL_EINVAL, "null argument");
+    const stencil_problem& g = job->global;
+    if (host_row < g.nx + 2 * g.radius || host_rows < g.ny + 2 * g.radius)
+        return set_error(STENCIL_EINVAL, "host array too small");
     if (int rc = sync_all(*job)) return rc;
-    const size_t es = job->global.dtype == STENCIL_F64 ? 8 : 4;
+    const size_t es = g.dtype == STENCIL_F64 ? 8 : 4;
     for (Slab& s : job->s) {
         if (int rc = set_dev(s.device)) return rc;
         // host planes [first, first + n + 2r) hold this slab's planes -r .. n+r-1
@@ -513,6 +560,35 @@ int stencil_slab_download(stencil_slab_job* job, void* host, int64_t host_row, i
         std::memcpy(static_cast<char*>(host) + size_t(s.first + z0 + r) * hplane, tmp.data() + size_t(z0 + r) * hplane,
                     size_t(z1 - z0) * hplane);
     }
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    if (int rc = sync_all(*job)) return rc;
+    if (int rc = set_dev(job->s[0].device)) return rc;
+    drop_timing(*job);
+    job->timing = enable != 0;
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,
+                             int32_t* signalled) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    if (int rc = sync_all(*job)) return rc;
+    if (int rc = set_dev(job->s[0].device)) return rc;
+    float sum = 0.f;
+    for (auto& e : job->tev) {
+        float ms = 0.f;
+        STENCIL_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
+        sum += ms;
+    }
+    if (total_ms) *total_ms = sum;
+    if (launches) *launches = int64_t(job->tev.size());
+    if (cells_per_launch) *cells_per_launch = job->timed_cells;
+    if (signalled) *signalled = job->signal ? 1 : 0;
     clear_error();
     return STENCIL_OK;
 }

@@ -75,7 +75,7 @@ class JacobiEngine:
         self.depth = int(self.layout.zghost) if spec.dims == 3 else spec.radius
         self.fused = spec.fusable
         # sweeps one fused launch performs (the library's own launch plan):
-        # 3 (or 4) for the 7-point star (TEMPORALK), 2 for the 27-point box
+        # 4 or 5 for the 7-point star (TEMPORALK), 3 or 4 for the 27-point box
         self.fuse_steps = 1
         if self.fused:
             # sweeps per fused launch: the most sweeps stencil_iterate runs as one launch
@@ -93,7 +93,7 @@ class JacobiEngine:
         k = _lib.INIT_RANDOM if kind == "random" else _lib.INIT_REFERENCE
         _lib.check(self.lib.stencil_fill_initial(ctypes.byref(self.layout), ctypes.c_void_p(grid.data_ptr()), k,
                                                  ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), _stream_handle(stream)),
-                   "stencil_fill_initial")
+                   "stencil_fill_initial", lib=self.lib)
 
     def reset(self, kind: str = "reference", seed: int = 0) -> None:
         self.fill_initial(self.a, kind, seed)
@@ -103,18 +103,18 @@ class JacobiEngine:
     def sweep(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, stream=None) -> None:
         _lib.check(self.lib.stencil_sweep(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                           ctypes.c_void_p(dst.data_ptr()), begin, end, _stream_handle(stream)),
-                   "stencil_sweep")
+                   "stencil_sweep", lib=self.lib)
 
     def sweep2(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, stream=None) -> None:
         _lib.check(self.lib.stencil_sweep2(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, _stream_handle(stream)),
-                   "stencil_sweep2")
+                   "stencil_sweep2", lib=self.lib)
 
     def sweepk(self, src: torch.Tensor, dst: torch.Tensor, begin: int, end: int, steps: int, stream=None) -> None:
         """dst = S^steps(src) on [begin, end) in one launch (steps 1..5; box: 1..3)."""
         _lib.check(self.lib.stencil_sweepk(ctypes.byref(self.layout), ctypes.c_void_p(src.data_ptr()),
                                            ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
-                                           _stream_handle(stream)), "stencil_sweepk")
+                                           _stream_handle(stream)), "stencil_sweepk", lib=self.lib)
 
     def sweepk_geometry(self, steps: int, begin: int = 0, end: int | None = None) -> dict:
         """How sweepk(steps) over [begin, end) would launch the K-step strip
@@ -122,7 +122,7 @@ class JacobiEngine:
         wg, zc, packed = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)
         end = self.slow_extent if end is None else end
         _lib.check(self.lib.stencil_sweepk_geometry(ctypes.byref(self.layout), begin, end, steps, ctypes.byref(wg),
-                                                    ctypes.byref(zc), ctypes.byref(packed)), "stencil_sweepk_geometry")
+                                                    ctypes.byref(zc), ctypes.byref(packed)), "stencil_sweepk_geometry", lib=self.lib)
         return {"workgroups": int(wg.value), "zchunk": int(zc.value), "packed": bool(packed.value)}
 
     @property
@@ -144,7 +144,7 @@ class JacobiEngine:
                                                   ctypes.c_void_p(dst.data_ptr()), begin, end, steps,
                                                   ctypes.c_void_p(counters.data_ptr()),
                                                   face_signal.ptr if face_signal is not None else None,
-                                                  ctypes.byref(n), _stream_handle(stream)), "stencil_sweepk_signal")
+                                                  ctypes.byref(n), _stream_handle(stream)), "stencil_sweepk_signal", lib=self.lib)
         return int(n.value)
 
     def face_signal(self) -> "FaceSignal":
@@ -155,7 +155,7 @@ class JacobiEngine:
         counters[1] >= target_hi (counters[2] is set on a 10 s timeout)."""
         _lib.check(self.lib.stencil_wait_counters(ctypes.c_void_p(counters.data_ptr()), target_lo, target_hi,
                                                   ctypes.c_void_p(counters.data_ptr() + 8), _stream_handle(stream)),
-                   "stencil_wait_counters")
+                   "stencil_wait_counters", lib=self.lib)
 
     def iterate(self, iterations: int, stream=None, timed: bool = False):
         """Whole job a -> ... ; returns (final grid tensor, device ms or None)."""
@@ -164,7 +164,7 @@ class JacobiEngine:
         _lib.check(self.lib.stencil_iterate(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
                                             ctypes.c_void_p(self.b.data_ptr()), iterations, _stream_handle(stream),
                                             ctypes.byref(fin), ctypes.byref(ms) if timed else None),
-                   "stencil_iterate")
+                   "stencil_iterate", lib=self.lib)
         return (self.b if fin.value else self.a), (ms.value if timed else None)
 
     def prepare(self, stream=None) -> None:
@@ -172,13 +172,13 @@ class JacobiEngine:
         z-chunk schedule trial) by one fused launch a -> b; `a` is unchanged."""
         _lib.check(self.lib.stencil_prepare(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
                                             ctypes.c_void_p(self.b.data_ptr()), _stream_handle(stream)),
-                   "stencil_prepare")
+                   "stencil_prepare", lib=self.lib)
 
     def plan(self, iterations: int):
         launches = ctypes.c_int64(0)
         kernel = ctypes.c_int32(0)
         _lib.check(self.lib.stencil_plan(ctypes.byref(self.layout), iterations, ctypes.byref(launches),
-                                         ctypes.byref(kernel)), "stencil_plan")
+                                         ctypes.byref(kernel)), "stencil_plan", lib=self.lib)
         return int(launches.value), int(kernel.value)
 
     # ----------------------------------------------------------------- views
@@ -195,14 +195,15 @@ class JacobiEngine:
     def interior(self, grid: torch.Tensor) -> torch.Tensor:
         """Strided (nz, ny, nx) / (ny, nx) view of the interior."""
         p, lay = self.prob, self.layout
+        base = grid.storage_offset()  # as_strided offsets are absolute in the storage
         if self.spec.dims == 3:
-            return grid.as_strided((p.nz, p.ny, p.nx), (lay.plane, lay.row, 1), lay.origin)
-        return grid.as_strided((p.ny, p.nx), (lay.row, 1), lay.origin)
+            return grid.as_strided((p.nz, p.ny, p.nx), (lay.plane, lay.row, 1), base + lay.origin)
+        return grid.as_strided((p.ny, p.nx), (lay.row, 1), base + lay.origin)
 
     def with_ghosts(self, grid: torch.Tensor) -> torch.Tensor:
         """Strided view of interior + ghost ring, the oracle's dense shape."""
         p, lay, r = self.prob, self.layout, self.r
-        corner = lay.origin - r * lay.row - r - (r * lay.plane if self.spec.dims == 3 else 0)
+        corner = grid.storage_offset() + lay.origin - r * lay.row - r - (r * lay.plane if self.spec.dims == 3 else 0)
         if self.spec.dims == 3:
             return grid.as_strided((p.nz + 2 * r, p.ny + 2 * r, p.nx + 2 * r), (lay.plane, lay.row, 1), corner)
         return grid.as_strided((p.ny + 2 * r, p.nx + 2 * r), (lay.row, 1), corner)
@@ -216,8 +217,79 @@ class JacobiEngine:
         out = np.zeros(self.slow_extent, dtype=np.float64)
         _lib.check(self.lib.stencil_plane_sums(ctypes.byref(self.layout), ctypes.c_void_p(grid.data_ptr()),
                                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-                                               _stream_handle(stream)), "stencil_plane_sums")
+                                               _stream_handle(stream)), "stencil_plane_sums", lib=self.lib)
         return out
+
+
+class RollingGrid:
+    """ONE resident grid plus `shift` spare planes (stencil_rolling_*): the
+    job stencil_iterate runs on two grids, bitwise, for grids whose two
+    copies do not fit the GPU (BASELINE config 3: 4096^3 fp32)."""
+
+    def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int, shift: int, device: int | torch.device = 0):
+        self.lib = _lib.load()
+        self.spec = spec
+        self.prob = spec.problem(nx, ny, nz)
+        self.layout = _lib.make_layout(self.prob)
+        self.device = torch.device("cuda", device) if isinstance(device, int) else device
+        self.shift = int(shift)
+        nbytes, k = ctypes.c_int64(0), ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_rolling_bytes(ctypes.byref(self.layout), self.shift, ctypes.byref(nbytes),
+                                                  ctypes.byref(k)), "stencil_rolling_bytes", lib=self.lib)
+        self.bytes, self.sweeps_per_pass = int(nbytes.value), int(k.value)
+        es = spec.elem_bytes
+        self.buf = torch.empty(-(-self.bytes // es), dtype=_TORCH_DTYPE[self.prob.dtype], device=self.device)
+        self.position = 0  # 0: the grid is at home (slot offset shift), 1: shifted to the allocation's start
+        self._grid_elems = int(self.layout.elems) + 256 // es
+        self._eng = JacobiEngine(spec, nx, ny, nz, device=self.device, allocate=False)
+
+    @staticmethod
+    def bytes_needed(spec: StencilSpec, nx: int, ny: int, nz: int, shift: int) -> int:
+        lib = _lib.load()
+        lay = _lib.make_layout(spec.problem(nx, ny, nz))
+        nbytes = ctypes.c_int64(0)
+        _lib.check(lib.stencil_rolling_bytes(ctypes.byref(lay), shift, ctypes.byref(nbytes), None),
+                   "stencil_rolling_bytes", lib=lib)
+        return int(nbytes.value)
+
+    @property
+    def grid(self) -> torch.Tensor:
+        """The current grid, as a tensor in the engine layout."""
+        start = 0 if self.position else self.shift * int(self.layout.plane)
+        return self.buf[start:start + self._grid_elems]
+
+    def reset(self, kind: str = "reference", seed: int = 0, stream=None) -> None:
+        self.position = 0
+        self._eng.fill_initial(self.grid, kind, seed, stream)
+        self.init_margin(stream)
+
+    def init_margin(self, stream=None) -> None:
+        _lib.check(self.lib.stencil_rolling_init_margin(ctypes.byref(self.layout), ctypes.c_void_p(self.buf.data_ptr()),
+                                                        self.shift, _stream_handle(stream)),
+                   "stencil_rolling_init_margin", lib=self.lib)
+
+    def iterate(self, iterations: int, stream=None, timed: bool = False):
+        """`iterations` sweeps; returns (current grid, device ms or None, launches)."""
+        pos = ctypes.c_int32(self.position)
+        n, ms = ctypes.c_int64(0), ctypes.c_float(0.0)
+        _lib.check(self.lib.stencil_rolling_iterate(ctypes.byref(self.layout), ctypes.c_void_p(self.buf.data_ptr()),
+                                                    self.shift, iterations, ctypes.byref(pos), _stream_handle(stream),
+                                                    ctypes.byref(n), ctypes.byref(ms) if timed else None),
+                   "stencil_rolling_iterate", lib=self.lib)
+        self.position = int(pos.value)
+        return self.grid, (ms.value if timed else None), int(n.value)
+
+    def interior(self, grid: torch.Tensor | None = None) -> torch.Tensor:
+        return self._eng.interior(self.grid if grid is None else grid)
+
+    def with_ghosts(self, grid: torch.Tensor | None = None) -> torch.Tensor:
+        return self._eng.with_ghosts(self.grid if grid is None else grid)
+
+    def to_numpy(self) -> np.ndarray:
+        return self._eng.to_numpy(self.grid)
+
+    def plane_sums(self, stream=None) -> np.ndarray:
+        return self._eng.plane_sums(self.grid, stream)
 
 
 class FaceSignal:
@@ -228,18 +300,18 @@ class FaceSignal:
     def __init__(self):
         self.lib = _lib.load()
         self.ptr = ctypes.c_void_p()
-        _lib.check(self.lib.stencil_face_signal_create(ctypes.byref(self.ptr)), "stencil_face_signal_create")
+        _lib.check(self.lib.stencil_face_signal_create(ctypes.byref(self.ptr)), "stencil_face_signal_create", lib=self.lib)
 
     def reset(self, stream=None) -> None:
-        _lib.check(self.lib.stencil_face_signal_reset(self.ptr, _stream_handle(stream)), "stencil_face_signal_reset")
+        _lib.check(self.lib.stencil_face_signal_reset(self.ptr, _stream_handle(stream)), "stencil_face_signal_reset", lib=self.lib)
 
     def wait(self, target: int, stream=None) -> None:
         _lib.check(self.lib.stencil_wait_face_signal(self.ptr, ctypes.c_uint64(target), _stream_handle(stream)),
-                   "stencil_wait_face_signal")
+                   "stencil_wait_face_signal", lib=self.lib)
 
     def value(self) -> int:
         v = ctypes.c_uint64(0)
-        _lib.check(self.lib.stencil_face_signal_read(self.ptr, ctypes.byref(v)), "stencil_face_signal_read")
+        _lib.check(self.lib.stencil_face_signal_read(self.ptr, ctypes.byref(v)), "stencil_face_signal_read", lib=self.lib)
         return int(v.value)
 
     def close(self) -> None:
@@ -262,9 +334,9 @@ def copy_bandwidth(nbytes: int, reps: int = 20, device: int = 0) -> float:
     src.fill_(1.0)
     ms = ctypes.c_float(0.0)
     _lib.check(lib.stencil_copy_bandwidth(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
-                                          nbytes, 2, _stream_handle(None), ctypes.byref(ms)), "copy warmup")
+                                          nbytes, 2, _stream_handle(None), ctypes.byref(ms)), "copy warmup", lib=lib)
     _lib.check(lib.stencil_copy_bandwidth(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
-                                          nbytes, reps, _stream_handle(None), ctypes.byref(ms)), "copy")
+                                          nbytes, reps, _stream_handle(None), ctypes.byref(ms)), "copy", lib=lib)
     return 2.0 * nbytes * reps / (ms.value * 1e-3) / 1e9
 
 
@@ -285,7 +357,7 @@ class SlabJob:
         kind = _lib.EXCHANGE_RCCL if exchange == "rccl" else _lib.EXCHANGE_COPY
         _lib.check(self.lib.stencil_slab_create(ctypes.byref(prob), len(devices), devs, kind,
                                                 _lib.SLAB_PERIODIC if periodic else 0, ctypes.byref(job)),
-                   "stencil_slab_create")
+                   "stencil_slab_create", lib=self.lib)
         self.job = job
         self.nslabs = len(devices)
 
@@ -304,13 +376,13 @@ class SlabJob:
         first, planes = ctypes.c_int64(0), ctypes.c_int64(0)
         dev, k = ctypes.c_int32(0), ctypes.c_int32(0)
         _lib.check(self.lib.stencil_slab_info(self.job, slab, ctypes.byref(first), ctypes.byref(planes),
-                                              ctypes.byref(dev), ctypes.byref(k)), "stencil_slab_info")
+                                              ctypes.byref(dev), ctypes.byref(k)), "stencil_slab_info", lib=self.lib)
         return {"first": int(first.value), "planes": int(planes.value), "device": int(dev.value),
                 "sweeps_per_round": int(k.value)}
 
     def fill_initial(self, kind: str = "reference", seed: int = 0) -> None:
         k = _lib.INIT_RANDOM if kind == "random" else _lib.INIT_REFERENCE
-        _lib.check(self.lib.stencil_slab_fill_initial(self.job, k, seed), "stencil_slab_fill_initial")
+        _lib.check(self.lib.stencil_slab_fill_initial(self.job, k, seed), "stencil_slab_fill_initial", lib=self.lib)
 
     def _dense(self) -> np.ndarray:
         nx, ny, nz = self.shape
@@ -321,23 +393,35 @@ class SlabJob:
     def upload(self, dense: np.ndarray) -> None:
         a = np.ascontiguousarray(dense)
         _lib.check(self.lib.stencil_slab_upload(self.job, ctypes.c_void_p(a.ctypes.data), a.shape[2], a.shape[1]),
-                   "stencil_slab_upload")
+                   "stencil_slab_upload", lib=self.lib)
 
     def download(self) -> np.ndarray:
         """The current global grid, dense with ghosts (oracle layout)."""
         a = self._dense()
         _lib.check(self.lib.stencil_slab_download(self.job, ctypes.c_void_p(a.ctypes.data), a.shape[2], a.shape[1]),
-                   "stencil_slab_download")
+                   "stencil_slab_download", lib=self.lib)
         return a
 
     def run(self, iterations: int) -> float:
         """`iterations` sweeps; returns the host wall time of the rounds (ms)."""
         ms = ctypes.c_float(0.0)
-        _lib.check(self.lib.stencil_slab_run(self.job, iterations, ctypes.byref(ms)), "stencil_slab_run")
+        _lib.check(self.lib.stencil_slab_run(self.job, iterations, ctypes.byref(ms)), "stencil_slab_run", lib=self.lib)
         return float(ms.value)
+
+    def kernel_timing(self, enable: bool) -> None:
+        """Record hipEvents around slab 0's compute launch of every round from
+        now on (the whole slab in face-signalled rounds, else its interior)."""
+        _lib.check(self.lib.stencil_slab_kernel_timing(self.job, 1 if enable else 0), "stencil_slab_kernel_timing", lib=self.lib)
+
+    def kernel_time(self) -> dict:
+        ms, n, cells, sig = ctypes.c_float(0.0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_slab_kernel_time(self.job, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(cells),
+                                                     ctypes.byref(sig)), "stencil_slab_kernel_time", lib=self.lib)
+        return {"total_ms": float(ms.value), "launches": int(n.value), "cells_per_launch": int(cells.value),
+                "signalled": bool(sig.value)}
 
     def plane_sums(self) -> np.ndarray:
         out = np.zeros(self.shape[2], dtype=np.float64)
         _lib.check(self.lib.stencil_slab_plane_sums(self.job, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
-                   "stencil_slab_plane_sums")
+                   "stencil_slab_plane_sums", lib=self.lib)
         return out

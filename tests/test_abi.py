@@ -106,7 +106,7 @@ def test_error_strings():
 
 
 def test_plan_counts_launches(monkeypatch):
-    lib = _lib.load()
+    lib = _lib.load(debug=True)  # STENCIL_NO_TK below is an experiment knob
     lay2 = _lib.make_layout(_lib.make_problem(dims=2, nx=64, ny=64))
     launches, kernel = ctypes.c_int64(), ctypes.c_int32()
     assert lib.stencil_plan(ctypes.byref(lay2), 100, ctypes.byref(launches), ctypes.byref(kernel)) == 0
@@ -140,3 +140,24 @@ def test_plan_counts_launches(monkeypatch):
     lay = _lib.make_layout(_lib.make_problem(dims=3, radius=2, nx=8, ny=8, nz=8))
     assert lib.stencil_plan(ctypes.byref(lay), 7, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 7 and kernel.value == _lib.KERNEL_DIRECT
+
+
+def test_product_library_ignores_experiment_knobs(monkeypatch):
+    """The shipped library runs AUTO's plan only: experiment knobs (here
+    STENCIL_NO_TK, which turns the K-step kernel off) are read by the debug
+    twin alone; the documented STENCIL_TK_STEPS is read by both."""
+    prod, dbg = _lib.load(debug=False), _lib.load(debug=True)
+    assert prod.stencil_debug_knobs() == 0 and dbg.stencil_debug_knobs() == 1
+    lay = _lib.make_layout(_lib.make_problem(dims=3, nx=8, ny=8, nz=8))
+    launches, kernel = ctypes.c_int64(), ctypes.c_int32()
+    monkeypatch.setenv("STENCIL_NO_TK", "1")
+    assert _lib.load() is dbg  # an experiment knob is set: the debug twin
+    assert prod.stencil_plan(ctypes.byref(lay), 8, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert (launches.value, kernel.value) == (2, _lib.KERNEL_TEMPORALK)
+    assert dbg.stencil_plan(ctypes.byref(lay), 8, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert (launches.value, kernel.value) == (4, _lib.KERNEL_TEMPORAL2)
+    monkeypatch.delenv("STENCIL_NO_TK")
+    monkeypatch.setenv("STENCIL_TK_STEPS", "3")
+    assert _lib.load() is prod  # documented knobs keep the product
+    assert prod.stencil_plan(ctypes.byref(lay), 9, ctypes.byref(launches), ctypes.byref(kernel)) == 0
+    assert launches.value == 3

@@ -1,0 +1,121 @@
+"""One resident grid (stencil_rolling_*): the job stencil_iterate runs on two
+ping-pong grids (the reference's two owner buffers, stencil.cpp:14-21,
+88-92), run in place with D spare planes, bitwise against the oracle and
+against the two-grid path -- up to BASELINE config 3 itself, 4096^3 fp32 on
+one GPU, where two grids do not fit."""
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+pytestmark = pytest.mark.gpu
+
+
+def same_bits(a, b):
+    return a.shape == b.shape and np.array_equal(np.ascontiguousarray(a).view(np.uint8),
+                                                 np.ascontiguousarray(b).view(np.uint8))
+
+
+def spec(dtype, shape="star", r=1, kernel="auto"):
+    from stencil_amd.engine import StencilSpec
+    return StencilSpec(dims=3, dtype=dtype, shape=shape, radius=r, order="naive", kernel=kernel)
+
+
+@pytest.mark.parametrize("dtype,shape,r,dims3", [
+    ("fp64", "star", 1, (131, 61, 29)),   # K = 4
+    ("fp32", "star", 1, (200, 90, 23)),   # K = 4 (small planes)
+    ("fp32", "star", 1, (1024, 1024, 9)), # K = 5 (fp32 planes >= 1024^2: C3's kernel)
+    ("fp64", "box", 1, (77, 40, 19)),     # K = 3
+    ("fp64", "box", 1, (700, 650, 11)),   # K = 4 (fp64 box planes >= 640^2)
+    ("fp64", "star", 2, (45, 23, 17)),    # single sweeps (direct kernel)
+])
+def test_rolling_matches_oracle(gpu, dtype, shape, r, dims3):
+    """Every shift from the minimum (K + 1: one-plane launches) to more than
+    the grid (one launch per pass), iteration counts with remainder passes,
+    zero iterations, repeated calls continuing from the returned position."""
+    from stencil_amd.engine import RollingGrid
+    nx, ny, nz = dims3
+    sp = spec(dtype, shape, r)
+    p = ob.problem(3, dtype, shape, r, "naive", nx, ny, nz)
+    probe = RollingGrid(sp, nx, ny, 1, 64, device=gpu)  # (the pass depth of this problem)
+    k = probe.sweeps_per_pass
+    del probe
+    iters = sorted({0, 1, 2, k, k + 1, 2 * k + 3})
+    for shift in (k + 1, k + 3, nz + k + 5):
+        g = RollingGrid(sp, nx, ny, nz, shift, device=gpu)
+        for it in iters:
+            g.reset("random", 90 + it)
+            g.iterate(it)
+            assert same_bits(g.to_numpy(), ob.run(p, it, "random", 90 + it, threads=16)), (shift, it)
+        # continuing: 3 then 4 more sweeps == 7 sweeps
+        g.reset("random", 5)
+        g.iterate(3)
+        g.iterate(4)
+        assert same_bits(g.to_numpy(), ob.run(p, 7, "random", 5, threads=16)), shift
+
+
+def test_rolling_equals_two_grids_c3_planes(gpu):
+    """4096^2 x 1024 fp32 7-point (C3's planes, a quarter of its depth), 40
+    sweeps from the reference initial condition: the rolling job with the
+    shift bench.py picks for C3 and the two-grid stencil_iterate, bitwise."""
+    import torch
+    from stencil_amd.engine import JacobiEngine, RollingGrid
+    nx = ny = 4096
+    nz, it = 1024, 40
+    sp = spec("fp32")
+    e = JacobiEngine(sp, nx, ny, nz, device=gpu)
+    e.reset()
+    fin, _ = e.iterate(it)
+    want = e.interior(fin).clone()
+    del e, fin
+    torch.cuda.empty_cache()
+    g = RollingGrid(sp, nx, ny, nz, 395, device=gpu)
+    assert g.sweeps_per_pass == 5
+    g.reset()
+    _, _, launches = g.iterate(it)
+    assert launches == 8 * 3  # 8 passes of ceil(1024 / 390) launches
+    assert torch.equal(g.interior(), want)
+    del g, want
+    torch.cuda.empty_cache()
+
+
+def test_c3_full_size_on_one_gpu(gpu):
+    """BASELINE config 3 at its stated size, 4096^3 fp32 7-point, on ONE GPU
+    (two grids would need 2 x 279 GB): 10 sweeps of the rolling job from the
+    reference initial condition.  Size-independent checks against the
+    two-grid path on a 4096^2 x 64 grid: after t = 10 sweeps plane z depends
+    on planes z-10 .. z+10 only, so the deep grid's bottom 54 planes equal the
+    shallow grid's bottom 54, its top 54 the shallow grid's top 54, and every
+    plane in [10, nz - 10) the shallow grid's plane 32 -- bit for bit (whole
+    planes compared on the GPU); plus the bitwise x-mirror symmetry of the
+    reference initial condition."""
+    import torch
+    from stencil_amd.engine import JacobiEngine, RollingGrid
+    nx = ny = 4096
+    it = 10
+    sp = spec("fp32")
+    e = JacobiEngine(sp, nx, ny, 64, device=gpu)
+    e.reset()
+    fin, _ = e.iterate(it)
+    ref = e.interior(fin).clone()  # 64 planes, 4.3 GB
+    del e, fin
+    torch.cuda.empty_cache()
+    nz = 4096
+    free = torch.cuda.mem_get_info(gpu)[0]
+    lay_plane = RollingGrid.bytes_needed(sp, nx, ny, 1, 64) - RollingGrid.bytes_needed(sp, nx, ny, 1, 63)
+    grid_bytes = RollingGrid.bytes_needed(sp, nx, ny, nz, 6)
+    shift = int(min(400, (free - grid_bytes - (2 << 30)) // lay_plane + 6))
+    assert shift >= 40, f"free {free / 2**30:.1f} GiB leaves no room for the rolling margin"
+    g = RollingGrid(sp, nx, ny, nz, shift, device=gpu)
+    g.reset()
+    g.iterate(it)
+    got = g.interior()
+    assert torch.equal(got[:54], ref[:54])
+    assert torch.equal(got[nz - 54:], ref[64 - 54:])
+    mid = ref[32]
+    for z in range(10, nz - 10, 1):
+        assert torch.equal(got[z], mid), z
+    assert torch.equal(got[100], torch.flip(got[100], dims=[1]))
+    assert float(got.min()) >= 0.0 and float(got.max()) <= 1.0
+    del g, got, ref
+    torch.cuda.empty_cache()

@@ -133,3 +133,54 @@ def test_slab_job_rejects_bad_requests(gpu):
     with pytest.raises(_lib.StencilError):
         SlabJob(StencilSpec(dims=2), 32, 32, 1, devices=[gpu], exchange="copy")
     assert _lib.EXCHANGE_COPY == 1
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs at least 2 GPUs (one slab per distinct device)")
+@pytest.mark.parametrize("ndev", [2, 4, 8])
+@pytest.mark.parametrize("exchange", ["copy", "rccl"])
+@pytest.mark.parametrize("signal", ["1", "0"])
+@pytest.mark.parametrize("shape_name", ["star", "box"])
+def test_slab_job_distinct_gpus(gpu, monkeypatch, ndev, exchange, signal, shape_name):
+    """Slabs on DISTINCT GPUs -- cross-device RCCL send/recv, hipMemcpyPeerAsync
+    with cross-device event waits, face-signalled rounds with N > 1 -- bitwise
+    equal to one undivided grid on GPU 0 (runs only where >= 2 GPUs are
+    visible: the driver's 8-GPU node, never the one-GPU test box)."""
+    if _device_count() < ndev:
+        pytest.skip(f"needs {ndev} GPUs")
+    monkeypatch.setenv("STENCIL_SLAB_SIGNAL", signal)
+    spec = StencilSpec(dims=3, dtype="fp64", shape=shape_name)
+    shape = (131, 61, 12 * ndev + 5)
+    job = SlabJob(spec, *shape, devices=list(range(ndev)), exchange=exchange)
+    k = job.info(0)["sweeps_per_round"]
+    job.fill_initial("random", 31)
+    it = 3 * k + 2
+    job.run(it)
+    got = job.download()
+    job.close()
+    assert same_bits(got, single_grid(gpu, spec, shape, it, 31))
+
+
+def test_bench_single_process_slab_job_rehearsal(gpu):
+    """bench.py --gpus 2 without a launcher, rehearsed on one GPU (both slabs
+    on GPU 0, device-copy halos): the JSON line, its roofline from the slab
+    job's kernel events, and the bitwise check against the global grid."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-device",
+                        "--exchange", "copy", "--n", "128", "--steps", "16", "--warmup", "4"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["grid"] == [128, 128, 256]
+    assert line["multi_gpu_check"]["bitwise_equal"], line["multi_gpu_check"]
+    assert line["roofline"]["launches"] > 0 and line["roofline"]["frac"] > 0
+    assert "ONE process" in line["config"]["parallelism"]
