@@ -21,7 +21,8 @@ LIB := stencil_amd/libstencil_hip.so
 LIB_DBG := stencil_amd/libstencil_hip_debug.so
 CLI := build/bin/stencil_main
 SRCS := $(wildcard stencil_amd/csrc/*.hip)
-OBJS := $(patsubst stencil_amd/csrc/%.hip,build/obj/%.o,$(SRCS))
+# kernels_boxk_probe.hip is built twice: with and without SLP vectorisation
+OBJS := $(patsubst stencil_amd/csrc/%.hip,build/obj/%.o,$(SRCS)) build/obj/kernels_boxk_probe_noslp.o
 HOST_SRCS := $(wildcard stencil_amd/csrc/host/*.cpp)
 HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
 
@@ -38,6 +39,12 @@ build/obj/knobs.o: stencil_amd/csrc/knobs.cpp
 build/obj/knobs_debug.o: stencil_amd/csrc/knobs.cpp
 	@mkdir -p build/obj
 	$(CXX) -O2 -std=c++17 -fPIC -Wall -DSTENCIL_DEBUG_KNOBS -c $< -o $@
+
+build/obj/kernels_boxk_probe_noslp.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
+	@mkdir -p build/obj
+	$(HIPCC) $(HIPFLAGS) -DPROBE_NOSLP -fno-slp-vectorize -c $< -o $@
+
+build/obj/kernels_boxk_probe.o: stencil_amd/csrc/kernels_boxk.hip
 
 $(LIB): $(OBJS) build/obj/knobs.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) build/obj/knobs.o

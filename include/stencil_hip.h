@@ -259,8 +259,9 @@ int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* strea
  * reference swaps two owner buffers every sweep (src/stencil/stencil.cpp:
  * 14-21, 88-92; include/stencil/boundary_matrix.hpp:59); here a pass of K
  * fused sweeps writes plane z of the new grid into the slot D planes below
- * (down pass) or back (up pass), in launches over z-ranges of D - K planes
- * ordered so that no launch writes a slot any later read needs.  Results
+ * (down pass) or back (up pass), in launches over z-ranges of D - K*r planes
+ * ordered so that no launch writes a slot any later read needs (D >= K*r + 1;
+ * K = the sweeps of one pass, r = the radius).  Results
  * are bitwise those of stencil_iterate.
  *   allocation: stencil_rolling_bytes(l, D, &bytes, &K) bytes at `base`;
  *   the grid at home (position 0) is the layout's grid at base + D*plane*esz,

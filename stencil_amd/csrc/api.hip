@@ -725,11 +725,11 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
 // GB, more than one MI355X holds.  Here one grid plus D spare planes below it:
 // a pass of k fused sweeps writes plane z of the new grid into slot z - D
 // (down pass) or, from there, back into slot z (up pass), as ceil(nz / S)
-// launches over z-ranges of S = D - K planes (K = the deepest pass), taken
-// bottom-up on the down pass and top-down on the up pass.  A launch over
-// [jS, jS + S) reads slots [jS - k, jS + S + k) and writes slots
-// [jS - D, jS + S - D) (down): disjoint, and no later launch reads what it
-// writes; the up pass mirrors it.  Same kernels, same arithmetic: bitwise
+// launches over z-ranges of S = D - K*r planes (K = the deepest pass, r the
+// radius: a pass reads K*r planes beyond its range), taken bottom-up on the
+// down pass and top-down on the up pass.  A launch over [jS, jS + S) reads
+// slots [jS - kr, jS + S + kr) and writes slots [jS - D, jS + S - D) (down):
+// disjoint, and no later launch reads what it writes; the up pass mirrors it.  Same kernels, same arithmetic: bitwise
 // the two-grid job.  Slots are indexed from the home grid's interior plane 0:
 // the allocation holds slots [-D - zg, nz + zg), home = slot -zg.
 // ---------------------------------------------------------------------------
@@ -749,8 +749,10 @@ int check_rolling(const stencil_layout* l, int64_t shift) {
     const stencil_problem& p = l->prob;
     if (p.dims != 3) return set_error(STENCIL_EUNSUPPORTED, "rolling jobs cover 3D grids (z passes)");
     if (p.flags != 0) return set_error(STENCIL_EINVAL, "rolling jobs take no slab halo flags");
-    const int k = rolling_steps(p);
-    if (shift < k + 1) return set_error(STENCIL_EINVAL, "shift must be at least %d planes (got %lld)", k + 1, (long long)shift);
+    const int64_t reach = int64_t(rolling_steps(p)) * p.radius;  // planes a pass reads beyond its range
+    if (shift < reach + 1)
+        return set_error(STENCIL_EINVAL, "shift must be at least %lld planes (got %lld)", (long long)(reach + 1),
+                         (long long)shift);
     return STENCIL_OK;
 }
 
@@ -789,7 +791,7 @@ int stencil_rolling_iterate(const stencil_layout* l, void* base, int64_t shift_p
     const stencil_problem& p = l->prob;
     const int64_t nz = p.nz, zg = l->zghost, D = shift_planes;
     const int K = rolling_steps(p);
-    const int64_t S = D - K;
+    const int64_t S = D - int64_t(K) * p.radius;
     const size_t pe = size_t(l->plane) * elem_size(p);
     char* shifted = static_cast<char*>(base);
     char* home = shifted + size_t(D) * pe;

@@ -146,6 +146,12 @@ bool temporal2_supports(const stencil_problem& p);
 int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
                  int steps, hipStream_t s);
 bool box27_supports(const stencil_problem& p);
+// the fp32 one-cell-per-lane box strip shapes (cfg RRNN), compiled with and
+// without SLP vectorisation (kernels_boxk_probe.hip; debug cfgs 95RRNN / 96RRNN)
+int launch_boxk_probe_slp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                          int cfg, hipStream_t s);
+int launch_boxk_probe_noslp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                            int cfg, hipStream_t s);
 int launch_tb2d(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s);
 // the whole 2D job as one persistent launch (kernels_tb2dp.hip); EUNSUPPORTED
 // when the tiles do not all fit on the GPU at once

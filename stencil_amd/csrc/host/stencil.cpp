@@ -109,8 +109,13 @@ auto Stencil::run_slabs(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std
                               options.exchange_copy ? STENCIL_EXCHANGE_COPY : STENCIL_EXCHANGE_RCCL, 0, &job.j),
           "stencil_slab_create");
     check(stencil_slab_upload(job.j, matrix.data(), matrix.row_stride(), matrix.rows_with_boundary()), "slab upload");
-    if (options.iterations > 0) {  // untimed warm-up (code-object load, RCCL connection setup), then a fresh upload
-        check(stencil_slab_run(job.j, 1, nullptr), "slab warm-up");
+    if (options.iterations > 0) {
+        // untimed warm-up (code-object load, RCCL connection setup, the K-step
+        // path's one-time schedule choices): one full round of K fused sweeps
+        // and one shorter remainder round, then a fresh upload
+        int32_t k = 1;
+        check(stencil_slab_info(job.j, 0, nullptr, nullptr, nullptr, &k), "stencil_slab_info");
+        check(stencil_slab_run(job.j, uint32_t(std::min<int64_t>(options.iterations, k) + 1), nullptr), "slab warm-up");
         check(stencil_slab_upload(job.j, matrix.data(), matrix.row_stride(), matrix.rows_with_boundary()), "slab upload");
     }
     float ms = 0.f;

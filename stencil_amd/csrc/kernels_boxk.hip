@@ -92,7 +92,7 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_sep(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
               int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-              unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
+              unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int /*xcd_pw: strip only*/) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LY = Tl::LY, RW = Tl::RW;
@@ -351,7 +351,7 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_strip(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
                 int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig, const int* __restrict__ sched) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int xcd_pw) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW;
@@ -371,11 +371,30 @@ __global__ void __launch_bounds__(64 * NW)
         za = zbeg + e[1];
         zb = za + e[2];
     } else {
-        const int bz = t / (tiles_x * tiles_y);
-        za = zbeg + bz * zchunk;
-        zb = za + zchunk < zend ? za + zchunk : zend;
         nch = (zend - zbeg + zchunk - 1) / zchunk;
-        t -= bz * tiles_x * tiles_y;
+        if (!SIG && xcd_pw > 0) {
+            // XCD patches (experiment, STENCIL_BOXK_XCD = patch width): blocks
+            // b and b + 8 share an XCD (round-robin dispatch; speed only, the
+            // map is a bijection either way), so XCD b % 8 walks its own
+            // contiguous run of (chunk, tile) units in column strips of xcd_pw
+            // tiles -- the workgroups resident on one XCD at a time form a
+            // 2D patch whose shared halo rows / columns are L2 hits
+            const int64_t tiles = int64_t(tiles_x) * tiles_y, total = tiles * nch;
+            const int64_t per = (total + 7) / 8;
+            const int64_t u = int64_t(blockIdx.x % 8) * per + blockIdx.x / 8;
+            if (u >= total) return;  // whole workgroup, before any barrier
+            const int64_t c = u / tiles, tt = u - c * tiles;
+            const int64_t strip = tt / (int64_t(xcd_pw) * tiles_y);
+            const int64_t rem = tt - strip * xcd_pw * tiles_y;
+            const int64_t sw = tiles_x - strip * xcd_pw < xcd_pw ? tiles_x - strip * xcd_pw : xcd_pw;
+            t = int(rem / sw * tiles_x + strip * xcd_pw + rem % sw);
+            za = zbeg + int(c) * zchunk;
+        } else {
+            const int bz = t / (tiles_x * tiles_y);
+            za = zbeg + bz * zchunk;
+            t -= bz * tiles_x * tiles_y;
+        }
+        zb = za + zchunk < zend ? za + zchunk : zend;
     }
     const int bx = t % tiles_x;
     const int by = t / tiles_x;
@@ -675,12 +694,14 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
-    if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
+    if (nb > (int64_t(1) << 31) - 8) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
+    const int xcd_pw = STRIP && !SIG ? env_int("STENCIL_BOXK_XCD", 0) : 0;
     auto launch = [&](bool packed) {
-        hipLaunchKernelGGL(kern, dim3(unsigned(packed ? nb : nb_equal)), dim3(64, NW, 1), 0, s,
+        const int64_t n = packed ? nb : (xcd_pw > 0 ? (nb_equal + 7) / 8 * 8 : nb_equal);
+        hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
                            static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
                            int(gy), int(lo), int(hi), int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig,
-                           packed ? sched : nullptr);
+                           packed ? sched : nullptr, packed ? 0 : xcd_pw);
         return hipGetLastError();
     };
     if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
@@ -691,6 +712,7 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
 
 }  // namespace
 
+#ifndef BOXK_PROBE_TU  // kernels_boxk_probe.hip re-includes the kernels above only
 bool box27_supports(const stencil_problem& p) {
     return p.dims == 3 && p.shape == STENCIL_BOX && p.radius == 1 && p.order == STENCIL_ORDER_NAIVE;
 }
@@ -701,6 +723,11 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
     if (!box27_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "the box kernel supports the 3D r=1 naive 27-point box only");
     const int cfg = env_int("STENCIL_BOXK_CFG", 0);
+    // code-generation probe (debug library only): fp32 one cell
+    // per lane, built with (95xxxx) and without (96xxxx) SLP vectorisation
+    if (cfg >= 950000 && cfg < 970000 && l.prob.dtype == STENCIL_F32)
+        return cfg < 960000 ? launch_boxk_probe_slp(l, in, out, begin, end, steps, cfg % 10000, s)
+                            : launch_boxk_probe_noslp(l, in, out, begin, end, steps, cfg % 10000, s);
     // strip layout (box27_strip): cfg = 9VRRNN (V cells per lane, RR rows per wave, NN waves)
     if (cfg >= 900000) {
         if (l.prob.dtype == STENCIL_F32) {
@@ -866,5 +893,6 @@ int launch_box27(const stencil_layout& l, const void* in, void* out, int64_t beg
                  hipStream_t s) {
     return launch_boxk(l, in, out, begin, end, steps, s);
 }
+#endif  // BOXK_PROBE_TU
 
 }  // namespace stencil

@@ -120,7 +120,13 @@ struct StripTile {
 // (hipStreamWaitValue64) with no wait kernel resident during the launch.
 // NS: input planes in registers -- in(p-2) .. in(p+NS-3): loads are issued
 // NS-2 planes ahead (4: two planes).
-template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true>
+// HL: stage 1's two history planes t_1(q) live in LDS instead of registers --
+// each wave's own rows only (no barrier: a wave reads back what it wrote), so
+// LDS serves as per-wave register space: 28 VGPRs per lane fewer at RY = 7,
+// for 7 ds_write_b64 + 28 ds_read_b64 per wave and step, which pays for one
+// more fused sweep (K = 5) at the same 7-row strips.
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true,
+          bool HL = false>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
@@ -130,7 +136,10 @@ __global__ void __launch_bounds__(64 * NW)
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
     static_assert(TY > 0 && TX > 0, "tile too small for K");
     static_assert(RY >= 2, "a strip needs a first and a last row");
+    static_assert(!HL || K >= 2, "HL keeps stage 1's history");
     __shared__ __attribute__((aligned(16))) T L[NB][K][NW][2][RW];
+    // HL: t_1 history [plane parity][region row][x], each wave its own rows
+    __shared__ __attribute__((aligned(16))) T HLs[HL ? 2 : 1][HL ? RH : 1][HL ? RW : 1];
 
     // Work = the linearised (tile, z) space of the range, tile-major: units
     // [lo, hi) of it per workgroup.  zchunk > 0: fixed chunks of every tile;
@@ -238,7 +247,16 @@ __global__ void __launch_bounds__(64 * NW)
     constexpr int LCM = NS % 2 == 0 ? NS : 2 * NS;  // steps until ring slot and H parity repeat
     const int p0 = za - K;
     VT vin[NS][RY];                 // slot (q - p0) % NS holds in(q)
-    VT H[K > 1 ? K - 1 : 1][2][RY]; // H[s-1][(q - p0) & 1] holds t_s(q), s < K
+    VT H[K > 1 ? K - 1 : 1][2][RY]; // H[s-1][(q - p0) & 1] holds t_s(q), s < K (HL: s >= 2 only)
+    // t_s(q) of parity `par`, row k: stage 1 from LDS with HL, else registers
+    auto hget = [&](int s, int par, int k) -> VT {
+        if (HL && s == 1) return *reinterpret_cast<const VT*>(&HLs[par][w * RY + k][xl]);
+        return H[s - 1][par][k];
+    };
+    auto hset = [&](int s, int par, int k, const VT& v) {
+        if (HL && s == 1) *reinterpret_cast<VT*>(&HLs[par][w * RY + k][xl]) = v;
+        else H[s - 1][par][k] = v;
+    };
 #pragma unroll
     for (int i = 0; i < NS; ++i)
 #pragma unroll
@@ -292,11 +310,11 @@ __global__ void __launch_bounds__(64 * NW)
                     up = k == 0 ? STRIP_ABOVE(0) : vin[(S + NS - 1) % NS][k == 0 ? 0 : k - 1];
                     dn = k == RY - 1 ? STRIP_BELOW(0) : vin[(S + NS - 1) % NS][k == RY - 1 ? 0 : k + 1];
                 } else {
-                    c = H[s - 2][(S - s + 4) & 1][k];
-                    zm = H[s - 2][(S - s + 5) & 1][k];
+                    c = hget(s - 1, (S - s + 4) & 1, k);
+                    zm = hget(s - 1, (S - s + 5) & 1, k);
                     zp = prev;
-                    up = k == 0 ? STRIP_ABOVE(s - 1) : H[s - 2][(S - s + 4) & 1][k == 0 ? 0 : k - 1];
-                    dn = k == RY - 1 ? STRIP_BELOW(s - 1) : H[s - 2][(S - s + 4) & 1][k == RY - 1 ? 0 : k + 1];
+                    up = k == 0 ? STRIP_ABOVE(s - 1) : hget(s - 1, (S - s + 4) & 1, k == 0 ? 0 : k - 1);
+                    dn = k == RY - 1 ? STRIP_BELOW(s - 1) : hget(s - 1, (S - s + 4) & 1, k == RY - 1 ? 0 : k + 1);
                 }
                 const T wl = sdpp<kSShr1>(c[V - 1]);
                 const T er = sdpp<kSShl1>(c[0]);
@@ -314,7 +332,7 @@ __global__ void __launch_bounds__(64 * NW)
                     if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
                 }
                 // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
-                if constexpr (s >= 2) H[s - 2][(S - s + 5) & 1][k] = prev;
+                if constexpr (s >= 2) hset(s - 1, (S - s + 5) & 1, k, prev);
                 prev = o;
             };
             stage(std::integral_constant<int, 1>{});
@@ -341,8 +359,8 @@ __global__ void __launch_bounds__(64 * NW)
         *reinterpret_cast<VT*>(&L[P][0][w][1][xl]) = vin[S % NS][RY - 1];
 #pragma unroll
         for (int s = 2; s <= K; ++s) {  // t_{s-1}(p-s+1), now in H
-            *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = H[s - 2][(S - s + 5) & 1][0];
-            *reinterpret_cast<VT*>(&L[P][s - 1][w][1][xl]) = H[s - 2][(S - s + 5) & 1][RY - 1];
+            *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = hget(s - 1, (S - s + 5) & 1, 0);
+            *reinterpret_cast<VT*>(&L[P][s - 1][w][1][xl]) = hget(s - 1, (S - s + 5) & 1, RY - 1);
         }
         if constexpr (SIG) {
             // right after the store of a face's last plane (the host makes
@@ -413,18 +431,18 @@ __global__ void __launch_bounds__(64 * NW)
 int senv_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
-          bool FP = true>
+          bool FP = true, bool HL = false>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
-    static_assert(Tl::lds_bytes <= 160 * 1024, "LDS budget");
+    static_assert(Tl::lds_bytes + (HL ? size_t(2) * Tl::RH * Tl::RW * sizeof(T) : 0) <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP>;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP, HL>;
     const int64_t tiles = gx * gy;
     int dev = 0, slots = 0;
     STENCIL_HIP_CHECK(hipGetDevice(&dev));
@@ -766,6 +784,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 510608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
             case 610608: return launch_st<double, 1, 6, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
             case 610508: return launch_st<double, 1, 5, 8, 4, true, 0, false, 6>(l, in, out, begin, end, s);
+            // stage 1's history in LDS (HL): 8-row strips at K = 4
+            case 810808: return launch_st<double, 1, 8, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+            case 810708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
             }
         }
@@ -779,6 +800,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
         }
         switch (cfg) {
         case 10608: return launch_st<double, 1, 6, 8, 5>(l, in, out, begin, end, s);
+        // stage 1's history in LDS (HL): 7- and 8-row strips at K = 5
+        case 810708: return launch_st<double, 1, 7, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+        case 810608: return launch_st<double, 1, 6, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
         default: return launch_st<double, 1, 5, 8, 5>(l, in, out, begin, end, s);
         }
     }

@@ -275,7 +275,9 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
 
 @pytest.mark.parametrize("steps,strip", [("3", "1"), ("3", "416"), ("3", "10408"), ("3", "216"), ("3", "10808"),
                                          ("3", "20808"), ("4", "1"), ("4", "10708"), ("4", "10608"), ("4", "20708"),
-                                         ("5", "1"), ("5", "10608"), ("5", "20608")])
+                                         ("5", "1"), ("5", "10608"), ("5", "20608"),
+                                         # stage 1's history in LDS (HL)
+                                         ("4", "810808"), ("4", "810708"), ("5", "810708"), ("5", "810608")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])

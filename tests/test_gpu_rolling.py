@@ -41,7 +41,7 @@ def test_rolling_matches_oracle(gpu, dtype, shape, r, dims3):
     k = probe.sweeps_per_pass
     del probe
     iters = sorted({0, 1, 2, k, k + 1, 2 * k + 3})
-    for shift in (k + 1, k + 3, nz + k + 5):
+    for shift in (k * r + 1, k * r + 3, nz + k * r + 5):  # the minimum (one-plane launches) .. one launch per pass
         g = RollingGrid(sp, nx, ny, nz, shift, device=gpu)
         for it in iters:
             g.reset("random", 90 + it)
