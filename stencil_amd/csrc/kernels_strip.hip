@@ -130,7 +130,7 @@ template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool 
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast, int xcd_pw) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -157,7 +157,21 @@ __global__ void __launch_bounds__(64 * NW)
         lo = int64_t(e[0]) * nzr + e[1];
         hi = lo + e[2];
     } else if (zchunk > 0) {
-        const int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
+        int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
+        if (!SIG && xcd_pw > 0) {
+            // XCD patches (experiment, STENCIL_TK_XCD = patch width; as the box
+            // kernel's): XCD b % 8 walks its own run of (chunk, tile) units in
+            // column strips of xcd_pw tiles, so the workgroups resident on one
+            // XCD at a time form a 2D patch whose shared halo lines are L2 hits
+            const int64_t nch = (nzr + zchunk - 1) / zchunk, total = tiles * nch, per = (total + 7) / 8;
+            const int64_t u = int64_t(blockIdx.x % 8) * per + blockIdx.x / 8;
+            if (u >= total) return;  // whole workgroup, before any barrier
+            c = u / tiles;
+            const int64_t tt = u - c * tiles;
+            const int64_t strip = tt / (int64_t(xcd_pw) * tiles_y), rem = tt - strip * xcd_pw * tiles_y;
+            const int64_t sw = tiles_x - strip * xcd_pw < xcd_pw ? tiles_x - strip * xcd_pw : xcd_pw;
+            t = rem / sw * tiles_x + strip * xcd_pw + rem % sw;
+        }
         lo = t * nzr + c * zchunk;
         hi = lo + (zchunk < nzr - c * zchunk ? zchunk : nzr - c * zchunk);
         const int64_t nch = (nzr + zchunk - 1) / zchunk;
@@ -540,11 +554,13 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         info->steps = K;
         return STENCIL_OK;
     }
+    const int xcd_pw = !SIG && zc > 0 ? senv_int("STENCIL_TK_XCD", 0) : 0;
     auto launch = [&](bool packed) {
-        hipLaunchKernelGGL(kern, dim3(unsigned(packed ? nb : nb_equal)), dim3(64, NW, 1), 0, s,
+        const int64_t n = packed ? nb : (xcd_pw > 0 ? (nb_equal + 7) / 8 * 8 : nb_equal);
+        hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
                            static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
                            int(gy), int(lo), int(hi), avg_weight<T>(l.prob), sig, fsig, packed ? sched : nullptr,
-                           fast_of(packed));
+                           fast_of(packed), packed ? 0 : xcd_pw);
         return hipGetLastError();
     };
     if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
@@ -787,6 +803,8 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             // stage 1's history in LDS (HL): 8-row strips at K = 4
             case 810808: return launch_st<double, 1, 8, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             case 810708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+            // 9-row strips without the fast path: 72 rows for 64 output rows (512 = 8 x 64)
+            case 820908: return launch_st<double, 1, 9, 8, 4, true, 0, false, 4, false, true>(l, in, out, begin, end, s);
             default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
             }
         }
@@ -795,6 +813,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
         if (l.prob.dtype == STENCIL_F32) {
             switch (cfg) {
             case 20608: return launch_st<float, 2, 6, 8, 5>(l, in, out, begin, end, s);
+            // stage 1's history in LDS (HL): 6-row strips (226 VGPRs); 7 rows with one boundary buffer (254)
+            case 820608: return launch_st<float, 2, 6, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+            case 830708: return launch_st<float, 2, 7, 8, 5, false, 0, false, 4, true, true>(l, in, out, begin, end, s);
             default: return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
             }
         }
@@ -803,6 +824,8 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
         // stage 1's history in LDS (HL): 7- and 8-row strips at K = 5
         case 810708: return launch_st<double, 1, 7, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
         case 810608: return launch_st<double, 1, 6, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+        // + one boundary-row buffer (a second barrier per step) and no fast path: 7 rows fit (254 VGPRs)
+        case 830708: return launch_st<double, 1, 7, 8, 5, false, 0, false, 4, false, true>(l, in, out, begin, end, s);
         default: return launch_st<double, 1, 5, 8, 5>(l, in, out, begin, end, s);
         }
     }

@@ -277,7 +277,8 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
                                          ("3", "20808"), ("4", "1"), ("4", "10708"), ("4", "10608"), ("4", "20708"),
                                          ("5", "1"), ("5", "10608"), ("5", "20608"),
                                          # stage 1's history in LDS (HL)
-                                         ("4", "810808"), ("4", "810708"), ("5", "810708"), ("5", "810608")])
+                                         ("4", "810808"), ("4", "810708"), ("5", "810708"), ("5", "810608"),
+                                         ("4", "820908"), ("5", "830708"), ("5", "820608")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])
@@ -872,3 +873,25 @@ def test_cli_bmp_dump(gpu, tmp_path):
         row = data[54 + y * 152: 54 + y * 152 + 150]
         want = b"".join(bytes(heat(float(grid[y, x]))) for x in range(50))
         assert row == want, y
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+@pytest.mark.parametrize("pw", ["1", "3", "4"])
+@pytest.mark.parametrize("zchunk", ["0", "7"])
+def test_xcd_patch_tile_orders(gpu, monkeypatch, shape, pw, zchunk):
+    """The XCD-patch work orders (debug knobs STENCIL_TK_XCD / STENCIL_BOXK_XCD:
+    XCD b % 8 walks its own run of (chunk, tile) units in column strips of pw
+    tiles; the grid is rounded up to a multiple of 8 and surplus workgroups
+    leave at once) cover every (chunk, tile) unit exactly once: bitwise the
+    oracle on ragged grids of many tiles, with forced and automatic z-chunks."""
+    monkeypatch.setenv("STENCIL_TK_XCD" if shape == "star" else "STENCIL_BOXK_XCD", pw)
+    monkeypatch.setenv("STENCIL_TK_PACK", "0")
+    monkeypatch.setenv("STENCIL_TK_ZCHUNK" if shape == "star" else "STENCIL_BOXK_ZCHUNK", zchunk)
+    nx, ny, nz = 333, 250, 23
+    p = ob.problem(3, "fp64", shape, 1, "naive", nx, ny, nz)
+    e = engine(gpu, 3, "fp64", shape, 1, "naive", "auto", nx, ny, nz)
+    assert e.lib.stencil_debug_knobs() == 1
+    k = e.fuse_steps
+    e.reset("random", 61)
+    e.sweepk(e.a, e.b, 0, nz, k)
+    assert same_bits(e.to_numpy(e.b), ob.run(p, k, "random", 61, threads=16))
