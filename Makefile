@@ -8,8 +8,13 @@ JOBS ?= 8
 
 # -ffp-contract=off: no FMA contraction, the sum/multiply sequence must stay
 # the reference's.  Denormals are kept (no FTZ): diffusion fronts decay into
-# the denormal range in long runs.
-HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+# the denormal range in long runs.  -fno-slp-vectorize: the SLP
+# vectoriser pairs independent fp32 adds of different rows into v_pk_add_f32,
+# and in the fp32 one-cell-per-lane box shapes that code computes wrong
+# values (the same source without SLP is bitwise right); the
+# kernels' own vector types still give packed math within a lane.  Measured
+# equal or faster everywhere (fp32 box +6 %, profiles/r03/r03f_slp_ab.txt).
+HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize \
             -fno-gpu-flush-denormals-to-zero -Wall -Wno-pass-failed -Iinclude -Istencil_amd/csrc
 CXXFLAGS ?= -O2 -std=c++17 -Wall -Wextra -ffp-contract=off -Iinclude
 
@@ -21,36 +26,39 @@ LIB := stencil_amd/libstencil_hip.so
 LIB_DBG := stencil_amd/libstencil_hip_debug.so
 CLI := build/bin/stencil_main
 SRCS := $(wildcard stencil_amd/csrc/*.hip)
+OBJ ?= build/obj
 # kernels_boxk_probe.hip is built twice: with and without SLP vectorisation
-OBJS := $(patsubst stencil_amd/csrc/%.hip,build/obj/%.o,$(SRCS)) build/obj/kernels_boxk_probe_noslp.o
+OBJS := $(patsubst stencil_amd/csrc/%.hip,$(OBJ)/%.o,$(SRCS)) $(OBJ)/kernels_boxk_probe_noslp.o
 HOST_SRCS := $(wildcard stencil_amd/csrc/host/*.cpp)
 HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
 
 all: $(LIB) $(LIB_DBG) $(CLI) oracle
 
-build/obj/%.o: stencil_amd/csrc/%.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
-	@mkdir -p build/obj
+$(OBJ)/%.o: stencil_amd/csrc/%.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
+	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-build/obj/knobs.o: stencil_amd/csrc/knobs.cpp
-	@mkdir -p build/obj
+$(OBJ)/knobs.o: stencil_amd/csrc/knobs.cpp
+	@mkdir -p $(OBJ)
 	$(CXX) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-build/obj/knobs_debug.o: stencil_amd/csrc/knobs.cpp
-	@mkdir -p build/obj
+$(OBJ)/knobs_debug.o: stencil_amd/csrc/knobs.cpp
+	@mkdir -p $(OBJ)
 	$(CXX) -O2 -std=c++17 -fPIC -Wall -DSTENCIL_DEBUG_KNOBS -c $< -o $@
 
-build/obj/kernels_boxk_probe_noslp.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
-	@mkdir -p build/obj
+$(OBJ)/kernels_boxk_probe_noslp.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
+	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPROBE_NOSLP -fno-slp-vectorize -c $< -o $@
 
-build/obj/kernels_boxk_probe.o: stencil_amd/csrc/kernels_boxk.hip
+$(OBJ)/kernels_boxk_probe.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -fslp-vectorize -c $< -o $@
 
-$(LIB): $(OBJS) build/obj/knobs.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) build/obj/knobs.o
+$(LIB): $(OBJS) $(OBJ)/knobs.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(OBJ)/knobs.o
 
-$(LIB_DBG): $(OBJS) build/obj/knobs_debug.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) build/obj/knobs_debug.o
+$(LIB_DBG): $(OBJS) $(OBJ)/knobs_debug.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(OBJ)/knobs_debug.o
 
 $(CLI): $(HOST_SRCS) $(HOST_HDRS) $(LIB) include/stencil_hip.h
 	@mkdir -p build/bin

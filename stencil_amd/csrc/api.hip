@@ -196,32 +196,37 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 __device__ __forceinline__ void u01(uint64_t u, float& f) { f = float(u >> 40) * 0x1.0p-24f; }
 __device__ __forceinline__ void u01(uint64_t u, double& d) { d = double(u >> 11) * 0x1.0p-53; }
 
-// One thread per allocated element.  Padding columns (outside the ghost
-// ring) get 0; ghost cells follow stencil.cpp:190-207 generalised to 3D.
+// Every allocated element, grid-stride: a dispatch holds at most 2^32 - 1
+// work-items per dimension (the AQL packet's grid size is 32-bit), and a
+// 4096^3 fp32 grid has 17.5e9 elements -- a one-thread-per-element grid
+// would be truncated modulo 2^32 and leave most planes unfilled.  Padding
+// columns (outside the ghost ring) get 0; ghost cells follow
+// stencil.cpp:190-207 generalised to 3D.
 template <typename T>
 __global__ void fill_initial_kernel(T* __restrict__ buf, Geom g, int64_t elems, int64_t row,
                                     int64_t rows, int64_t origin_x, int r, int zg, int dims, int kind,
                                     uint64_t seed) {
-    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= elems) return;
-    const int64_t pz = i / (row * rows);
-    const int64_t rem = i - pz * row * rows;
-    const int64_t py = rem / row;
-    const int64_t px = rem - py * row;
-    const int64_t x = px - origin_x, y = py - r, z = dims == 3 ? pz - zg : 0;
-    T v = T(0);
-    const bool in_x = x >= -r && x < g.nx + r;
-    if (in_x) {
-        const bool xghost = x < 0 || x >= g.nx;
-        const bool interior = !xghost && y >= 0 && y < g.ny && z >= 0 && z < g.nz;
-        if (xghost) {
-            v = T(1);
-        } else if (interior && kind == STENCIL_INIT_RANDOM) {
-            const uint64_t lin = (uint64_t(z) * uint64_t(g.ny) + uint64_t(y)) * uint64_t(g.nx) + uint64_t(x);
-            u01(splitmix64(seed + lin), v);
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < elems;
+         i += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t pz = i / (row * rows);
+        const int64_t rem = i - pz * row * rows;
+        const int64_t py = rem / row;
+        const int64_t px = rem - py * row;
+        const int64_t x = px - origin_x, y = py - r, z = dims == 3 ? pz - zg : 0;
+        T v = T(0);
+        const bool in_x = x >= -r && x < g.nx + r;
+        if (in_x) {
+            const bool xghost = x < 0 || x >= g.nx;
+            const bool interior = !xghost && y >= 0 && y < g.ny && z >= 0 && z < g.nz;
+            if (xghost) {
+                v = T(1);
+            } else if (interior && kind == STENCIL_INIT_RANDOM) {
+                const uint64_t lin = (uint64_t(z) * uint64_t(g.ny) + uint64_t(y)) * uint64_t(g.nx) + uint64_t(x);
+                u01(splitmix64(seed + lin), v);
+            }
         }
+        buf[i] = v;
     }
-    buf[i] = v;
 }
 
 // Deterministic per-plane sums: one workgroup per slow-axis index, fixed
@@ -371,7 +376,7 @@ int stencil_fill_initial(const stencil_layout* l, void* dev, int init_kind, uint
     const Geom g = geom_of(*l);
     const int64_t r = l->prob.radius;
     const int64_t origin_x = l->origin - r * l->row - l->zghost * l->plane;
-    const int64_t blocks = (l->elems + 255) / 256;
+    const int64_t blocks = std::min<int64_t>((l->elems + 255) / 256, int64_t(1) << 22);  // <= 2^30 work-items
     if (l->prob.dtype == STENCIL_F32)
         hipLaunchKernelGGL(fill_initial_kernel<float>, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream),
                            static_cast<float*>(dev), g, l->elems, l->row, l->rows, origin_x, int(r),

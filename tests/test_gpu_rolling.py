@@ -119,3 +119,38 @@ def test_c3_full_size_on_one_gpu(gpu):
     assert float(got.min()) >= 0.0 and float(got.max()) <= 1.0
     del g, got, ref
     torch.cuda.empty_cache()
+
+
+def test_fill_initial_beyond_2_32_elements(gpu):
+    """The initial-condition fill of a grid of more than 2^32 elements
+    (4096^2 x 300 fp32: 5.1e9 with ghosts and padding): every plane gets the
+    reference condition and the random interior matches the splitmix64 rule
+    at sampled cells of the last planes.  (A one-work-item-per-element
+    dispatch is truncated modulo 2^32 work-items: before round 3 the fill
+    left every plane past the first ~2^32 elements unset -- caught by the
+    rolling tests at C3 size.)"""
+    import torch
+    from stencil_amd.engine import JacobiEngine
+    nx, ny, nz = 4096, 4096, 300
+    e = JacobiEngine(spec("fp32"), nx, ny, nz, device=gpu, allocate=False)
+    assert int(e.layout.elems) > 2 ** 32
+    e.a = torch.full((int(e.layout.elems) + 64,), 7.0, dtype=torch.float32, device=torch.device("cuda", gpu))
+    e.fill_initial(e.a, "reference")
+    g = e.with_ghosts(e.a)
+    assert bool((g[:, :, 0] == 1).all()) and bool((g[:, :, -1] == 1).all())  # x-ghost faces, every plane
+    assert float(e.interior(e.a).abs().max()) == 0.0
+    assert float(g[:, 0, 1:-1].abs().max()) == 0.0 and float(g[-1, 1:-1, 1:-1].abs().max()) == 0.0
+    e.fill_initial(e.a, "random", 5)
+    inner = e.interior(e.a)
+    m64 = (1 << 64) - 1
+
+    def splitmix(x):
+        z = (x + 0x9E3779B97F4A7C15) & m64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m64
+        return z ^ (z >> 31)
+    for z, y, x in ((nz - 1, ny - 1, nx - 1), (nz - 1, 17, 4000), (299, 2048, 0), (150, 3, 5)):
+        want = float(np.float32((splitmix(5 + (z * ny + y) * nx + x) >> 40) * 2.0 ** -24))
+        assert float(inner[z, y, x]) == want, (z, y, x)
+    del e, g, inner
+    torch.cuda.empty_cache()
