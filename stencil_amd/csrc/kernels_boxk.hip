@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(64 * NW)
     } else {
         nch = (zend - zbeg + zchunk - 1) / zchunk;
         if (!SIG && xcd_pw > 0) {
-            // XCD patches (experiment, STENCIL_BOXK_XCD = patch width): blocks
+            // XCD patches (default 4 tiles wide; STENCIL_BOXK_XCD = width): blocks
             // b and b + 8 share an XCD (round-robin dispatch; speed only, the
             // map is a bijection either way), so XCD b % 8 walks its own
             // contiguous run of (chunk, tile) units in column strips of xcd_pw
@@ -695,7 +695,12 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 8) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
-    const int xcd_pw = STRIP && !SIG ? env_int("STENCIL_BOXK_XCD", 0) : 0;
+    // XCD-patch work order for equal-chunk strip launches: 2048^2 x 256 fp64
+    // K = 4 cuts L2-miss reads from 18.6 to 10.6 GB per launch (2.16x -> 1.23x
+    // compulsory) and the launch time by 3 % (6.12 -> 5.93 ms; widths 2 / 8:
+    // 6.01 / 5.96; profiles/r03/r03d_ab_box_xcd.txt) -- the kernel is bound by
+    // its fp64 VALU work, not by those bytes
+    const int xcd_pw = STRIP && !SIG ? env_int("STENCIL_BOXK_XCD", 4) : 0;
     auto launch = [&](bool packed) {
         const int64_t n = packed ? nb : (xcd_pw > 0 ? (nb_equal + 7) / 8 * 8 : nb_equal);
         hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
