@@ -281,7 +281,7 @@ def main():
         grid.iterate(args.warmup)
         barrier()
         t0 = time.perf_counter()
-        _, dev_ms, kernel_launches = grid.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)
+        dev_ms, kernel_launches = grid.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)[1:]
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         kernel_ms_total = dev_ms

@@ -38,6 +38,9 @@
 
 #include "common.hpp"
 
+#ifndef BOX_FAST_PATH
+#define BOX_FAST_PATH 1
+#endif
 
 namespace stencil {
 namespace {
@@ -92,7 +95,8 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_sep(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
               int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-              unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int /*xcd_pw: strip only*/) {
+              unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int /*xcd_pw: strip only*/,
+              int /*fast: strip only*/) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, LY = Tl::LY, RW = Tl::RW;
@@ -351,7 +355,7 @@ template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
     box27_strip(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk, int tiles_x,
                 int tiles_y, int halo_lo, int halo_hi, int ld_lo, int ld_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int xcd_pw) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int xcd_pw, int fast) {
     using Tl = BKTile<T, V, RY, NW, K>;
     using VT = typename VecB<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW;
@@ -433,6 +437,9 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
+    // the whole region inside the grid in x and y (the fast path's condition)
+    const bool xy_inner = fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
+                          int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny;
     // R = (l + c) + r and E = l + r of a row vector (x-neighbours by DPP)
     auto sums = [&](const VT& v, VT& R, VT& E) {
         const T wl = bdpp<kShr1>(v[V - 1]);
@@ -488,8 +495,9 @@ __global__ void __launch_bounds__(64 * NW)
 #pragma unroll
     for (int i = 0; i < 2; ++i) load_plane(vin[i], p0 + i);
 
-    auto step = [&](auto S_, int p) {
+    auto stepb = [&](auto S_, int p, auto FAST_) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % 4
+        constexpr bool FAST = decltype(FAST_)::value;  // every stage plane and the region inside: no ghost selects
         constexpr int PW = S & 1, PR = PW ^ 1;  // LDS buffer written / read this step
         __syncthreads();
         const int zo = p - 2 * K;  // t_K(zo) -> HBM this step
@@ -529,7 +537,7 @@ __global__ void __launch_bounds__(64 * NW)
                         P9p[s - 1][k][j] = p9;
                     }
                     o[j] = fin * avg;
-                    if (s < K) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cq1(k)[j];
+                    if (s < K && !FAST) o[j] = (zin && yin[k] && xin[j]) ? o[j] : cq1(k)[j];
                 }
                 if constexpr (s == K) {
                     if (do_store && st[k]) {
@@ -589,6 +597,24 @@ __global__ void __launch_bounds__(64 * NW)
         *reinterpret_cast<VT*>(&L[PW][0][w][0][xl]) = rsum(vin[S][0]);
         *reinterpret_cast<VT*>(&L[PW][0][w][1][xl]) = rsum(vin[S][RY - 1]);
         load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
+    };
+
+    // interior steps skip the intermediate stages' ghost-cell selects (as the
+    // 7-point strip kernel's fast path): the region inside the grid in x and
+    // y, every intermediate stage plane inside its computed z range
+    auto step = [&](auto S_, int p) {
+        if constexpr (!BOX_FAST_PATH || SIG) {
+            stepb(S_, p, std::false_type{});
+        } else {
+            bool all_in = xy_inner;
+#pragma unroll
+            for (int s = 1; s < K; ++s) {
+                const int m = zr(p - 2 * s);
+                all_in = all_in && m >= (halo_lo ? -(K - s) : 0) && m < (halo_hi ? nz + (K - s) : nz);
+            }
+            if (all_in) stepb(S_, p, std::true_type{});
+            else stepb(S_, p, std::false_type{});
+        }
     };
 
     const int plast = zb - 1 + 2 * K;
@@ -706,7 +732,7 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
                            static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
                            int(gy), int(lo), int(hi), int(ld_lo), int(ld_hi), avg_weight<T>(l.prob), sig, fsig,
-                           packed ? sched : nullptr, packed ? 0 : xcd_pw);
+                           packed ? sched : nullptr, packed ? 0 : xcd_pw, env_int("STENCIL_BOXK_FAST", 1));
         return hipGetLastError();
     };
     if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);

@@ -58,8 +58,11 @@ def test_rolling_equals_two_grids_c3_planes(gpu):
     """4096^2 x 1024 fp32 7-point (C3's planes, a quarter of its depth), 40
     sweeps from the reference initial condition: the rolling job with the
     shift bench.py picks for C3 and the two-grid stencil_iterate, bitwise."""
+    import gc
     import torch
     from stencil_amd.engine import JacobiEngine, RollingGrid
+    gc.collect()
+    torch.cuda.empty_cache()  # earlier tests' cached blocks: this test needs ~210 GB
     nx = ny = 4096
     nz, it = 1024, 40
     sp = spec("fp32")
@@ -89,8 +92,11 @@ def test_c3_full_size_on_one_gpu(gpu):
     plane in [10, nz - 10) the shallow grid's plane 32 -- bit for bit (whole
     planes compared on the GPU); plus the bitwise x-mirror symmetry of the
     reference initial condition."""
+    import gc
     import torch
     from stencil_amd.engine import JacobiEngine, RollingGrid
+    gc.collect()
+    torch.cuda.empty_cache()  # earlier tests' cached blocks: this test needs the whole HBM
     nx = ny = 4096
     it = 10
     sp = spec("fp32")
@@ -116,7 +122,8 @@ def test_c3_full_size_on_one_gpu(gpu):
     for z in range(10, nz - 10, 1):
         assert torch.equal(got[z], mid), z
     assert torch.equal(got[100], torch.flip(got[100], dims=[1]))
-    assert float(got.min()) >= 0.0 and float(got.max()) <= 1.0
+    # values in [0, 1] (every plane of `got` is bitwise one of `ref`'s, checked above)
+    assert float(ref.min()) >= 0.0 and float(ref.max()) <= 1.0
     del g, got, ref
     torch.cuda.empty_cache()
 
