@@ -4,9 +4,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|NS]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Two multi-GPU drivers, same job, same JSON line:
+Multi-GPU drivers, same job, same JSON line:
   * one process per GPU (launched by torch.distributed.run; WORLD_SIZE set):
-    stencil_amd/slab.py over torch.distributed (RCCL);
+    the C-ABI rank-mode slab job (stencil_slab_create_rank: each rank its own
+    slab, RCCL between the ranks); --driver python (or a rehearsal transport)
+    runs stencil_amd/slab.py over torch.distributed instead;
   * --gpus N without a launcher (WORLD_SIZE unset): ONE process drives the N
     GPUs through the C-ABI slab job (stencil_slab_*, csrc/slab.hip; RCCL
     ncclCommInitAll), the shape of the reference's single spawn/join of its
@@ -106,6 +108,9 @@ def parse():
                          "without a launcher, copy = device copies between the slabs (hipMemcpyPeerAsync)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal: every rank / slab uses GPU 0 (needs --exchange host, or copy without a launcher)")
+    ap.add_argument("--driver", default="auto", choices=["auto", "cabi", "python"],
+                    help="under torch.distributed.run: the C-ABI rank-mode slab job (auto/cabi) or the Python slab "
+                         "driver over torch.distributed (python; auto picks it for the rehearsal transports)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
@@ -223,6 +228,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if rank_job_wanted(args, world):
+        return main_rank_job(args, world, rank, local)
     # 1 process, 1 GPU, the structure of an interior rank: halos = own
     # boundary planes (periodic), by device copies or by RCCL send/recv to self
     loop = args.exchange in ("loopback", "nccl-self")
@@ -398,9 +405,23 @@ def main():
                workload_key=f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else
                ("C3_rolling_4096" if rolling else f"{args.config}_slab_{count}"),
                local=local, check=(check if world > 1 else None), cpu=(world == 1 and not loop),
-               extra_config={"rolling": rolling_info} if rolling else None)
+               extra_config={"rolling": rolling_info} if rolling else None,
+               kernels_per_launch=(kernel_launches / max(1.0, args.steps / sweeps_per_launch)) if rolling else 1.0)
     if world > 1 or args.exchange == "nccl-self":
         dist.destroy_process_group()
+
+
+def rank_job_wanted(args, world: int) -> bool:
+    """Under torch.distributed.run with N > 1: the C-ABI rank-mode job unless
+    --driver python or a rehearsal transport asks for the Python slab driver."""
+    if world <= 1 or args.driver == "python":
+        return False
+    if args.exchange != "nccl" or args.share_device or args.no_signal or args.face_signal or args.no_overlap:
+        if args.driver == "cabi":
+            raise SystemExit("--driver cabi: RCCL between distinct GPUs, default rounds (drop --exchange / "
+                             "--share-device / --no-signal / --face-signal / --no-overlap, or use --driver python)")
+        return False
+    return True
 
 
 def slab_job_plan(args, visible: int):
@@ -423,6 +444,109 @@ def slab_job_plan(args, visible: int):
     return list(range(n)), "rccl" if args.exchange == "nccl" else "copy"
 
 
+def global_grid_check(spec, grid, sweeps, got, device):
+    """The multi-GPU job's per-plane sums `got` against the same sweeps of the
+    global grid run as ONE grid on `device`, bit for bit (skipped when the
+    global grid does not fit beside the job)."""
+    import numpy as np
+    import torch
+
+    from stencil_amd.engine import JacobiEngine
+    gnx, gny, gnz = grid
+    try:
+        need = 2.2 * gnx * gny * gnz * spec.elem_bytes
+        free = torch.cuda.mem_get_info(device)[0]
+        if need > 0.9 * free:
+            return {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free on GPU {device}"}
+        ref = JacobiEngine(spec, gnx, gny, gnz, device=device)
+        ref.reset("reference")
+        fin, _ = ref.iterate(sweeps)
+        want = ref.plane_sums(fin)
+        bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
+        del ref, fin
+        torch.cuda.empty_cache()
+        return {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad, "bitwise_equal": bad == 0,
+                "reference": f"the global grid as one grid on GPU {device}, same sweeps, per-plane sums"}
+    except Exception as exc:  # a check, never the measurement
+        return {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
+
+def main_rank_job(args, world, rank, local):
+    """One process per GPU (torch.distributed.run) through the C-ABI rank-mode
+    slab job (stencil_slab_unique_id / stencil_slab_create_rank, csrc/slab.hip):
+    each rank builds and runs only its own z-slab, the halos over RCCL between
+    the ranks' slabs, face-signalled rounds -- the shape of an MPI-per-rank
+    launch.  torch.distributed (gloo, host side only) hands rank 0's RCCL id to
+    the others and carries the barriers, the max-over-ranks time and the
+    per-plane sums of the check; it moves no halo data."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from stencil_amd.engine import SlabJob, StencilSpec
+
+    pre = PRESETS[args.config]
+    if world < pre["min_gpus"]:
+        raise SystemExit(f"--config {args.config} needs at least {pre['min_gpus']} GPUs (grid memory)")
+    dist.init_process_group("gloo")
+    n = args.n
+    gnx, gny, gnz = (n, n, n * world) if pre["grid"] is None else pre["grid"]
+    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
+    uid = [SlabJob.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    job = SlabJob(spec, gnx, gny, gnz, [local], rank=(world, rank, uid[0]))
+    info = job.info(0)
+    k = info["sweeps_per_round"]
+    job.fill_initial("reference")
+    sweeps = k + 1 + args.warmup
+    job.run(k + 1)  # a full and a remainder round: both launch paths' one-time costs
+    job.run(args.warmup)
+    dist.barrier()
+    elapsed = job.run(args.steps) * 1e-3  # this rank's rounds, its device synchronised at both ends
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    sweeps += args.steps
+    extra = k * max(4, min(args.steps // max(1, k), 8))
+    job.kernel_timing(True)
+    job.run(extra)
+    kt = job.kernel_time()
+    job.kernel_timing(False)
+    sweeps += extra
+    check = None
+    if not args.no_check:
+        sums = job.plane_sums()  # this rank's planes filled in, the rest zero
+        mine = torch.from_numpy(sums[info["first"]:info["first"] + info["planes"]].copy())
+        width = gnz // world + 1
+        buf = torch.zeros(width, dtype=torch.float64)
+        buf[:mine.numel()] = mine
+        parts = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        counts = [None] * world
+        dist.all_gather_object(counts, info["planes"])
+        job.close()
+        if rank == 0:
+            got = np.concatenate([parts[r].numpy()[:counts[r]] for r in range(world)])
+            check = global_grid_check(spec, (gnx, gny, gnz), sweeps, got, local)
+        dist.barrier()
+    else:
+        job.close()
+    if rank == 0:
+        kname = "boxk" if spec.shape == "box" else "temporalk"
+        parallelism = (f"z-slab x{world}, one process per GPU (torch.distributed.run) through the C-ABI rank-mode "
+                       "slab job (stencil_slab_create_rank), RCCL send/recv between the ranks' slabs")
+        report(args, pre, spec, kname, (gnx, gny, gnz), world, elapsed, kt["total_ms"] / max(1, kt["launches"]),
+               float(kt["cells_per_launch"]), k, kt["launches"], parallelism,
+               rounds="one face-signalled launch per round" if kt["signalled"] else
+               "boundary + interior launches per round",
+               launch_timing="hipEvents around rank 0's " + ("whole-slab face-signalled" if kt["signalled"] else
+                                                             "interior") + " launches of extra rounds after the timed region",
+               workload_key=f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else
+               f"{args.config}_slab_{info['planes']}",
+               local=local, check=check, cpu=False)
+    dist.destroy_process_group()
+
+
 def main_slab_job(args):
     """--gpus N without a launcher: ONE process drives N GPUs through the C-ABI
     slab job (stencil_slab_create/run/plane_sums, csrc/slab.hip): z-slabs, one
@@ -432,10 +556,9 @@ def main_slab_job(args):
     driver; the roofline from hipEvents on slab 0's compute stream over extra
     rounds after the timed region; multi_gpu_check against the global grid run
     as one grid on GPU 0."""
-    import numpy as np
     import torch
 
-    from stencil_amd.engine import JacobiEngine, SlabJob, StencilSpec
+    from stencil_amd.engine import SlabJob, StencilSpec
 
     devices, exchange = slab_job_plan(args, torch.cuda.device_count())
     n_gpus = args.gpus
@@ -461,24 +584,7 @@ def main_slab_job(args):
     sweeps += extra
     check = None
     if not args.no_check:
-        got = job.plane_sums()
-        try:
-            need = 2.2 * gnx * gny * gnz * spec.elem_bytes
-            free = torch.cuda.mem_get_info(0)[0]
-            if need > 0.9 * free:
-                check = {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free on GPU 0"}
-            else:
-                ref = JacobiEngine(spec, gnx, gny, gnz, device=0)
-                ref.reset("reference")
-                fin, _ = ref.iterate(sweeps)
-                want = ref.plane_sums(fin)
-                bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
-                check = {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad, "bitwise_equal": bad == 0,
-                         "reference": "the global grid as one grid on GPU 0, same sweeps, per-plane sums"}
-                del ref, fin
-                torch.cuda.empty_cache()
-        except Exception as exc:  # a check, never the measurement
-            check = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+        check = global_grid_check(spec, (gnx, gny, gnz), sweeps, job.plane_sums(), 0)
     job.close()
     kname = "boxk" if spec.shape == "box" else "temporalk"
     where = "GPU 0 shared by every slab (rehearsal)" if args.share_device else f"{n_gpus} GPUs"
@@ -494,14 +600,17 @@ def main_slab_job(args):
 
 
 def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
-           kernel_launches, parallelism, rounds, launch_timing, workload_key, local, check, cpu, extra_config=None):
+           kernel_launches, parallelism, rounds, launch_timing, workload_key, local, check, cpu, extra_config=None,
+           kernels_per_launch=1.0):
     """Print the one JSON line.  Roofline of the dominant kernel: one launch
     advances its cells by `sweeps_per_launch` fused sweeps; its compulsory HBM
     traffic is one read plus one write of those cells (2 * sizeof(T) per cell,
     whatever K is): `achieved` = compulsory bytes / mean launch time, a true
     fraction of the HBM peak.  The per-sweep algorithmic figure of SURVEY
     8(d) (2 * sizeof(T) per cell-UPDATE, K per cell per launch) is
-    `effective_GBps`."""
+    `effective_GBps`.  kernels_per_launch: kernel launches per charged
+    "launch" (a rolling pass runs several z-range launches; the PMC table
+    holds bytes per kernel launch)."""
     from stencil_amd.engine import copy_bandwidth
     gnx, gny, gnz = grid
     total_updates = float(gnx) * gny * gnz * args.steps
@@ -512,6 +621,8 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
     achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9
     effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
     traffic, traffic_entry = load_traffic(workload_key, kname)
+    if traffic:
+        traffic = traffic * kernels_per_launch
     desc = pre["desc"].format(n=args.n)
     out = {
         "metric": METRIC,

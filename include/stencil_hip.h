@@ -328,6 +328,22 @@ typedef struct stencil_slab_job stencil_slab_job;
  * (NULL = 0 .. ngpus-1).  Every slab must own at least K planes. */
 int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange,
                         int32_t flags, stencil_slab_job** job);
+/* Rank mode: one process per GPU, as the reference's MPI-style launch and
+ * torch.distributed.run give it.  Rank 0 makes an RCCL id
+ * (stencil_slab_unique_id, STENCIL_SLAB_ID_BYTES bytes) and hands it to every
+ * rank by its own channel (a torch.distributed broadcast, MPI_Bcast, a file);
+ * each rank then calls stencil_slab_create_rank with the same global problem
+ * and builds only its slab (z split as above, slab = rank) on `device`, joined
+ * by ncclCommInitRank -- a collective: every rank must call it.  The job then
+ * holds ONE slab (stencil_slab_info slab 0) and every call below is
+ * per-rank and collective over the ranks (run: every rank the same
+ * iterations).  Host arrays keep the global shape: upload reads and download /
+ * plane_sums write only this rank's planes (download: plus the global ghost
+ * planes at the two ends).  Exchange is always RCCL. */
+enum { STENCIL_SLAB_ID_BYTES = 128 };
+int stencil_slab_unique_id(void* id, int64_t bytes);
+int stencil_slab_create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int32_t device,
+                             const void* id, int64_t id_bytes, int32_t flags, stencil_slab_job** job);
 int stencil_slab_destroy(stencil_slab_job* job);
 int stencil_slab_info(const stencil_slab_job* job, int32_t slab, int64_t* first_plane, int64_t* planes,
                       int32_t* device, int32_t* sweeps_per_round);

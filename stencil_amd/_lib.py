@@ -27,6 +27,7 @@ INIT_REFERENCE, INIT_RANDOM = 0, 1
 HALO_LO, HALO_HI = 1, 2
 EXCHANGE_RCCL, EXCHANGE_COPY = 0, 1
 SLAB_PERIODIC = 1
+SLAB_ID_BYTES = 128
 
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2,
                 "temporalk": KERNEL_TEMPORALK, "persistent": KERNEL_PERSISTENT}
@@ -45,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "stencil_face_signal_reset", "stencil_face_signal_read", "stencil_wait_face_signal",
     "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
     "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
-    "stencil_slab_kernel_timing", "stencil_slab_kernel_time",
+    "stencil_slab_kernel_timing", "stencil_slab_kernel_time", "stencil_slab_unique_id", "stencil_slab_create_rank",
 )
 
 
@@ -145,6 +146,9 @@ def load(debug: bool | None = None) -> ctypes.CDLL:
         "stencil_slab_create": (c_int, [POINTER(Problem), c_int32, POINTER(c_int32), c_int32, c_int32,
                                         POINTER(c_void_p)]),
         "stencil_slab_destroy": (c_int, [c_void_p]),
+        "stencil_slab_unique_id": (c_int, [c_void_p, c_int64]),
+        "stencil_slab_create_rank": (c_int, [POINTER(Problem), c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
+                                             POINTER(c_void_p)]),
         "stencil_slab_info": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32),
                                       POINTER(c_int32)]),
         "stencil_slab_fill_initial": (c_int, [c_void_p, c_int32, c_uint64]),

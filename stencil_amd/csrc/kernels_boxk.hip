@@ -38,8 +38,14 @@
 
 #include "common.hpp"
 
+// The interior fast path (no ghost selects on steps whose region lies inside
+// the grid) is compiled out: with it the 2048^2 x 256 box ran 24-28 % slower
+// (fp64 K = 4 695 -> 530, fp32 K = 3 1398 -> 1011 Gcell/s,
+// profiles/r03/r03h_ab_box*.txt), a second copy of the step body the
+// compiler schedules worse.  -DBOX_FAST_PATH=1 builds it (debug knob
+// STENCIL_BOXK_FAST then selects it).
 #ifndef BOX_FAST_PATH
-#define BOX_FAST_PATH 1
+#define BOX_FAST_PATH 0
 #endif
 
 namespace stencil {

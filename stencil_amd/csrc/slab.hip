@@ -40,10 +40,13 @@ namespace {
 // ---- the few RCCL entry points used, resolved at run time -----------------
 typedef struct ncclComm* ncclComm_t;
 typedef enum { ncclSuccess = 0 } ncclResult_t;
+struct ncclUniqueId { char internal[128]; };  // NCCL_UNIQUE_ID_BYTES
 enum { ncclChar = 0, ncclUint8 = 1 };  // ncclDataType_t: bytes
 
 struct Rccl {
     ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
@@ -62,13 +65,15 @@ const Rccl& rccl() {
         if (!h) return;
         auto sym = [&](auto& f, const char* name) { f = reinterpret_cast<std::decay_t<decltype(f)>>(dlsym(h, name)); };
         sym(r.CommInitAll, "ncclCommInitAll");
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
         sym(r.CommDestroy, "ncclCommDestroy");
         sym(r.GroupStart, "ncclGroupStart");
         sym(r.GroupEnd, "ncclGroupEnd");
         sym(r.Send, "ncclSend");
         sym(r.Recv, "ncclRecv");
         sym(r.GetErrorString, "ncclGetErrorString");
-        r.ok = r.CommInitAll && r.CommDestroy && r.GroupStart && r.GroupEnd && r.Send && r.Recv && r.GetErrorString;
+        r.ok = r.CommInitAll && r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.GroupStart && r.GroupEnd && r.Send && r.Recv && r.GetErrorString;
     });
     return r;
 }
@@ -82,6 +87,7 @@ const Rccl& rccl() {
 
 struct Slab {
     int device = 0;
+    int index = 0;             // global slab index (= RCCL rank)
     int64_t first = 0, n = 0;  // global first plane, planes owned
     stencil_layout l{};
     void* a = nullptr;
@@ -107,6 +113,7 @@ struct stencil_slab_job {
     bool cur_is_a = true;
     bool chained = false;  // round events recorded since the last join
     bool signal = false;   // full rounds as face-signalled single launches
+    int nranks = 0;        // rank mode (stencil_slab_create_rank): slabs of the job, this process owns s[0]
     std::vector<stencil::Slab> s;
     // stencil_slab_kernel_timing: hipEvents around slab 0's compute launch of
     // every round (the whole slab in face-signalled rounds, else the interior)
@@ -164,12 +171,14 @@ int fuse_depth(const stencil_problem& p) {
     return 1;
 }
 
+// neighbours of global slab i (its RCCL peers)
+int slabs_total(const stencil_slab_job& j) { return j.nranks ? j.nranks : int(j.s.size()); }
 int lo_nb(const stencil_slab_job& j, int i) {
-    const int n = int(j.s.size());
+    const int n = slabs_total(j);
     return i > 0 ? i - 1 : (j.periodic ? n - 1 : -1);
 }
 int hi_nb(const stencil_slab_job& j, int i) {
-    const int n = int(j.s.size());
+    const int n = slabs_total(j);
     return i < n - 1 ? i + 1 : (j.periodic ? 0 : -1);
 }
 
@@ -192,7 +201,7 @@ int exchange(stencil_slab_job& j, bool use_a) {
             Slab& s = j.s[i];
             void* g = use_a ? s.a : s.b;
             const size_t bytes = size_t(d) * plane_bytes(s);
-            const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+            const int lo = lo_nb(j, s.index), hi = hi_nb(j, s.index);
             // sends and receives to one peer match in posting order: a slab
             // that is its own neighbour (periodic, N = 1) sends hi -> recv lo
             // first, then lo -> hi
@@ -210,8 +219,8 @@ int exchange(stencil_slab_job& j, bool use_a) {
         SLAB_NCCL_CHECK(r.GroupEnd());
         return STENCIL_OK;
     }
-    // device copies: slab i's A stream pulls its neighbours' faces once their
-    // round is complete (ev_join, recorded on their A streams after joining B)
+    // device copies (single-process jobs only: local = global index): slab i's
+    // A stream pulls its neighbours' faces once their round is complete (ev_join, recorded on their A streams after joining B)
     for (int i = 0; i < n; ++i) {
         Slab& s = j.s[i];
         if (int rc = set_dev(s.device)) return rc;
@@ -373,32 +382,21 @@ using namespace stencil;
 
 extern "C" {
 
-int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange_kind,
-                        int32_t flags, stencil_slab_job** job) {
-    if (!global || !job || ngpus < 1) return set_error(STENCIL_EINVAL, "null argument or ngpus < 1");
-    *job = nullptr;
-    stencil_problem g = *global;
-    if (g.dims != 3) return set_error(STENCIL_EUNSUPPORTED, "slab jobs split 3D grids along z");
-    if (g.halo != 0 || g.flags != 0) return set_error(STENCIL_EINVAL, "the global problem takes no halo / flags");
-    if (exchange_kind != STENCIL_EXCHANGE_RCCL && exchange_kind != STENCIL_EXCHANGE_COPY)
-        return set_error(STENCIL_EINVAL, "bad exchange kind %d", exchange_kind);
-    if (flags & ~STENCIL_SLAB_PERIODIC) return set_error(STENCIL_EINVAL, "bad slab flags %d", flags);
-    stencil_layout gl;
-    if (int rc = stencil_layout_init(&g, &gl)) return rc;
-    std::vector<int> devs(static_cast<size_t>(ngpus));
-    for (int i = 0; i < ngpus; ++i) devs[size_t(i)] = devices ? devices[i] : i;
-    if (exchange_kind == STENCIL_EXCHANGE_RCCL) {
-        for (int i = 0; i < ngpus; ++i)
-            for (int k = 0; k < i; ++k)
-                if (devs[size_t(i)] == devs[size_t(k)])
-                    return set_error(STENCIL_EINVAL, "RCCL needs one slab per GPU (device %d twice): use device copies",
-                                     devs[size_t(i)]);
-        if (!rccl().ok) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
-    }
+}  // extern "C"
+
+namespace stencil {
+namespace {
+
+// The slabs this process owns: global slab indices `idx` (of `total`) on
+// `devs`; the z split is the same in every process (planes total / N, the first
+// nz % N slabs one more), so each rank can build its own share alone.
+int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, const std::vector<int>& devs,
+              int32_t exchange_kind, int32_t flags, bool rank_mode, stencil_slab_job** out) {
     auto* j = new stencil_slab_job;
     j->global = g;
     j->exchange = exchange_kind;
     j->periodic = flags & STENCIL_SLAB_PERIODIC;
+    j->nranks = rank_mode ? total : 0;
     j->k = fuse_depth(g);
     j->depth = std::max<int>(j->k, g.radius);
     // face-signalled rounds where the K-step kernels have them (3D r = 1 naive
@@ -411,18 +409,20 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
         // and only with one slab per GPU: slabs sharing a GPU multiplex their
         // streams onto its few hardware queues, where a polling wait kernel
         // could sit in front of the launch another slab's wait is polling for
+        // (ranks each own one GPU: RCCL refuses two ranks on one device)
         bool distinct = true;
-        for (int i = 0; i < ngpus; ++i)
-            for (int k = 0; k < i; ++k) distinct = distinct && devs[size_t(i)] != devs[size_t(k)];
-        j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct &&
-                    !off;
+        for (size_t i = 0; i < devs.size(); ++i)
+            for (size_t k = 0; k < i; ++k) distinct = distinct && devs[i] != devs[k];
+        j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct && !off;
     }
-    const int64_t base = g.nz / ngpus, rem = g.nz % ngpus;
-    j->s.resize(size_t(ngpus));
+    const int64_t base = g.nz / total, rem = g.nz % total;
+    j->s.resize(idx.size());
     int rc = STENCIL_OK;
-    for (int i = 0; i < ngpus && rc == STENCIL_OK; ++i) {
-        Slab& s = j->s[size_t(i)];
-        s.device = devs[size_t(i)];
+    for (size_t li = 0; li < idx.size() && rc == STENCIL_OK; ++li) {
+        const int i = idx[li];
+        Slab& s = j->s[li];
+        s.index = i;
+        s.device = devs[li];
         s.n = base + (i < rem ? 1 : 0);
         s.first = i * base + std::min<int64_t>(i, rem);
         if (s.n < j->depth) {
@@ -449,18 +449,109 @@ int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int3
                                  hipMemset(s.counters, 0, 4 * sizeof(uint32_t)) != hipSuccess))
             rc = set_error(STENCIL_EHIP, "face counters on device %d", s.device);
     }
-    if (rc == STENCIL_OK && exchange_kind == STENCIL_EXCHANGE_RCCL) {
-        std::vector<ncclComm_t> comms(size_t(ngpus), nullptr);
-        const ncclResult_t e = rccl().CommInitAll(comms.data(), ngpus, devs.data());
-        if (e != ncclSuccess)
-            rc = set_error(STENCIL_EHIP, "ncclCommInitAll(%d) failed: %s", ngpus, rccl().GetErrorString(e));
-        else
-            for (int i = 0; i < ngpus; ++i) j->s[size_t(i)].comm = comms[size_t(i)];
-    }
     if (rc != STENCIL_OK) {
         release(j);
         return rc;
     }
+    *out = j;
+    return STENCIL_OK;
+}
+
+int check_global(const stencil_problem* global, stencil_problem* g, int32_t flags) {
+    *g = *global;
+    if (g->dims != 3) return set_error(STENCIL_EUNSUPPORTED, "slab jobs split 3D grids along z");
+    if (g->halo != 0 || g->flags != 0) return set_error(STENCIL_EINVAL, "the global problem takes no halo / flags");
+    if (flags & ~STENCIL_SLAB_PERIODIC) return set_error(STENCIL_EINVAL, "bad slab flags %d", flags);
+    stencil_layout gl;
+    return stencil_layout_init(g, &gl);
+}
+
+}  // namespace
+}  // namespace stencil
+
+extern "C" {
+
+int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange_kind,
+                        int32_t flags, stencil_slab_job** job) {
+    if (!global || !job || ngpus < 1) return set_error(STENCIL_EINVAL, "null argument or ngpus < 1");
+    *job = nullptr;
+    if (exchange_kind != STENCIL_EXCHANGE_RCCL && exchange_kind != STENCIL_EXCHANGE_COPY)
+        return set_error(STENCIL_EINVAL, "bad exchange kind %d", exchange_kind);
+    stencil_problem g;
+    if (int rc = check_global(global, &g, flags)) return rc;
+    std::vector<int> devs(static_cast<size_t>(ngpus)), idx(static_cast<size_t>(ngpus));
+    for (int i = 0; i < ngpus; ++i) {
+        devs[size_t(i)] = devices ? devices[i] : i;
+        idx[size_t(i)] = i;
+    }
+    if (exchange_kind == STENCIL_EXCHANGE_RCCL) {
+        for (int i = 0; i < ngpus; ++i)
+            for (int k = 0; k < i; ++k)
+                if (devs[size_t(i)] == devs[size_t(k)])
+                    return set_error(STENCIL_EINVAL, "RCCL needs one slab per GPU (device %d twice): use device copies",
+                                     devs[size_t(i)]);
+        if (!rccl().ok) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
+    }
+    stencil_slab_job* j = nullptr;
+    if (int rc = build_job(g, ngpus, idx, devs, exchange_kind, flags, false, &j)) return rc;
+    if (exchange_kind == STENCIL_EXCHANGE_RCCL) {
+        std::vector<ncclComm_t> comms(size_t(ngpus), nullptr);
+        const ncclResult_t e = rccl().CommInitAll(comms.data(), ngpus, devs.data());
+        if (e != ncclSuccess) {
+            const int rc = set_error(STENCIL_EHIP, "ncclCommInitAll(%d) failed: %s", ngpus, rccl().GetErrorString(e));
+            release(j);
+            return rc;
+        }
+        for (int i = 0; i < ngpus; ++i) j->s[size_t(i)].comm = comms[size_t(i)];
+    }
+    *job = j;
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_slab_unique_id(void* id, int64_t bytes) {
+    if (!id || bytes < int64_t(sizeof(ncclUniqueId)))
+        return set_error(STENCIL_EINVAL, "the id buffer needs %d bytes", int(sizeof(ncclUniqueId)));
+    if (!rccl().ok) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
+    ncclUniqueId u;
+    const ncclResult_t e = rccl().GetUniqueId(&u);
+    if (e != ncclSuccess) return set_error(STENCIL_EHIP, "ncclGetUniqueId failed: %s", rccl().GetErrorString(e));
+    std::memcpy(id, &u, sizeof(u));
+    clear_error();
+    return STENCIL_OK;
+}
+
+int stencil_slab_create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int32_t device,
+                             const void* id, int64_t id_bytes, int32_t flags, stencil_slab_job** job) {
+    if (!global || !job || !id) return set_error(STENCIL_EINVAL, "null argument");
+    *job = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(STENCIL_EINVAL, "rank %d of %d", rank, nranks);
+    if (id_bytes != int64_t(sizeof(ncclUniqueId)))
+        return set_error(STENCIL_EINVAL, "the id holds %d bytes, not %lld", int(sizeof(ncclUniqueId)),
+                         (long long)id_bytes);
+    stencil_problem g;
+    if (int rc = check_global(global, &g, flags)) return rc;
+    if (!rccl().ok) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
+    stencil_slab_job* j = nullptr;
+    if (int rc = build_job(g, nranks, {rank}, {device}, STENCIL_EXCHANGE_RCCL, flags, true, &j)) return rc;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    if (int rc = set_dev(device)) {
+        release(j);
+        return rc;
+    }
+    // collective over the ranks: every rank must reach it (a rank whose
+    // build_job failed returns before it, and the others wait in RCCL's own
+    // bootstrap until it times out)
+    const ncclResult_t e = rccl().CommInitRank(&comm, nranks, u, rank);
+    if (e != ncclSuccess) {
+        const int rc = set_error(STENCIL_EHIP, "ncclCommInitRank(%d of %d) failed: %s", rank, nranks,
+                                 rccl().GetErrorString(e));
+        release(j);
+        return rc;
+    }
+    j->s[0].comm = comm;
     *job = j;
     clear_error();
     return STENCIL_OK;
@@ -555,8 +646,8 @@ int stencil_slab_download(stencil_slab_job* job, void* host, int64_t host_row, i
         tmp.resize(size_t(s.n + 2 * r) * hplane);
         if (int rc = stencil_download(&s.l, job->cur_is_a ? s.a : s.b, tmp.data(), host_row, host_rows, s.sa)) return rc;
         STENCIL_HIP_CHECK(hipStreamSynchronize(s.sa));
-        const int64_t z0 = i == 0 ? -r : 0;
-        const int64_t z1 = i + 1 == job->s.size() ? s.n + r : s.n;
+        const int64_t z0 = s.index == 0 ? -r : 0;
+        const int64_t z1 = s.index + 1 == slabs_total(*job) ? s.n + r : s.n;
         std::memcpy(static_cast<char*>(host) + size_t(s.first + z0 + r) * hplane, tmp.data() + size_t(z0 + r) * hplane,
                     size_t(z1 - z0) * hplane);
     }

@@ -347,19 +347,41 @@ class SlabJob:
     per-process driver for callers without torch.distributed."""
 
     def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int, devices, exchange: str = "rccl",
-                 periodic: bool = False):
+                 periodic: bool = False, rank=None):
+        """rank=(nranks, rank, unique_id): rank mode (stencil_slab_create_rank),
+        this process's one slab on devices[0], the others in other processes
+        that make the same call with the same id (SlabJob.unique_id on one rank,
+        handed to the rest by the caller)."""
         self.lib = _lib.load()
         self.spec = spec
         self.shape = (nx, ny, nz)
         prob = spec.problem(nx, ny, nz)
-        devs = (ctypes.c_int32 * len(devices))(*devices)
         job = ctypes.c_void_p()
-        kind = _lib.EXCHANGE_RCCL if exchange == "rccl" else _lib.EXCHANGE_COPY
-        _lib.check(self.lib.stencil_slab_create(ctypes.byref(prob), len(devices), devs, kind,
-                                                _lib.SLAB_PERIODIC if periodic else 0, ctypes.byref(job)),
-                   "stencil_slab_create", lib=self.lib)
+        flags = _lib.SLAB_PERIODIC if periodic else 0
+        if rank is not None:
+            nranks, r, uid = rank
+            if exchange != "rccl" or len(devices) != 1:
+                raise ValueError("rank mode: one device per rank, RCCL exchange")
+            buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+            _lib.check(self.lib.stencil_slab_create_rank(ctypes.byref(prob), nranks, r, devices[0], buf, len(uid),
+                                                         flags, ctypes.byref(job)),
+                       "stencil_slab_create_rank", lib=self.lib)
+        else:
+            devs = (ctypes.c_int32 * len(devices))(*devices)
+            kind = _lib.EXCHANGE_RCCL if exchange == "rccl" else _lib.EXCHANGE_COPY
+            _lib.check(self.lib.stencil_slab_create(ctypes.byref(prob), len(devices), devs, kind, flags,
+                                                    ctypes.byref(job)),
+                       "stencil_slab_create", lib=self.lib)
         self.job = job
         self.nslabs = len(devices)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """A fresh RCCL id for a rank-mode job (make it on one rank only)."""
+        lib = _lib.load()
+        buf = ctypes.create_string_buffer(_lib.SLAB_ID_BYTES)
+        _lib.check(lib.stencil_slab_unique_id(buf, _lib.SLAB_ID_BYTES), "stencil_slab_unique_id", lib=lib)
+        return buf.raw
 
     def close(self) -> None:
         if self.job:

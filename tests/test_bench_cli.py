@@ -49,3 +49,29 @@ def test_bench_gpus_2_without_launcher_fails_clearly_without_gpus():
                        capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode != 0
     assert "--gpus 2 needs 2 GPUs, 0 visible" in p.stderr
+
+
+def rank_args(**kw):
+    base = dict(gpus=2, exchange="nccl", share_device=False, driver="auto", no_signal=False, face_signal=False,
+                no_overlap=False)
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+def test_torchrun_uses_the_cabi_rank_job_by_default():
+    """Under torch.distributed.run (N > 1) the default driver is the C-ABI
+    rank-mode slab job; one rank, --driver python and the rehearsal
+    transports keep the Python slab driver."""
+    assert bench.rank_job_wanted(rank_args(), 2)
+    assert bench.rank_job_wanted(rank_args(driver="cabi"), 8)
+    assert not bench.rank_job_wanted(rank_args(), 1)
+    assert not bench.rank_job_wanted(rank_args(driver="python"), 2)
+    assert not bench.rank_job_wanted(rank_args(exchange="host", share_device=True), 2)
+    assert not bench.rank_job_wanted(rank_args(no_signal=True), 2)
+
+
+def test_cabi_driver_refuses_rehearsal_transports():
+    with pytest.raises(SystemExit, match="--driver cabi"):
+        bench.rank_job_wanted(rank_args(driver="cabi", exchange="host"), 2)
+    with pytest.raises(SystemExit, match="--driver cabi"):
+        bench.rank_job_wanted(rank_args(driver="cabi", face_signal=True), 2)

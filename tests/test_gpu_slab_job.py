@@ -184,3 +184,73 @@ def test_bench_single_process_slab_job_rehearsal(gpu):
     assert line["multi_gpu_check"]["bitwise_equal"], line["multi_gpu_check"]
     assert line["roofline"]["launches"] > 0 and line["roofline"]["frac"] > 0
     assert "ONE process" in line["config"]["parallelism"]
+
+
+@pytest.mark.parametrize("shape_name", ["star", "box"])
+@pytest.mark.parametrize("periodic", [False, True])
+def test_rank_mode_single_rank(gpu, shape_name, periodic):
+    """Rank mode (stencil_slab_create_rank: ncclCommInitRank from an id made by
+    stencil_slab_unique_id) with one rank: non-periodic it is the plain grid;
+    as a periodic ring (the rank sends its faces to itself over RCCL) it equals
+    the single-process job's device-copy ring, bit for bit."""
+    spec = StencilSpec(dims=3, dtype="fp64", shape=shape_name)
+    shape = (64, 40, 30)
+    uid = SlabJob.unique_id()
+    assert len(uid) == 128
+    job = SlabJob(spec, *shape, devices=[gpu], periodic=periodic, rank=(1, 0, uid))
+    info = job.info(0)
+    assert info["first"] == 0 and info["planes"] == shape[2] and info["device"] == gpu
+    job.fill_initial("random", 5)
+    k = info["sweeps_per_round"]
+    job.run(2 * k + 1)
+    got = job.download()
+    sums = job.plane_sums()
+    job.close()
+    if periodic:
+        ref = SlabJob(spec, *shape, devices=[gpu], exchange="copy", periodic=True)
+        ref.fill_initial("random", 5)
+        ref.run(2 * k + 1)
+        want = ref.download()
+        want_sums = ref.plane_sums()
+        ref.close()
+    else:
+        want = single_grid(gpu, spec, shape, 2 * k + 1, 5)
+        e = JacobiEngine(spec, *shape, device=gpu)
+        e.reset("random", 5)
+        fin, _ = e.iterate(2 * k + 1)
+        want_sums = e.plane_sums(fin)
+    assert same_bits(got, want)
+    assert np.array_equal(sums, want_sums)
+
+
+def test_rank_mode_rejects_bad_requests(gpu):
+    from stencil_amd import _lib
+    spec = StencilSpec(dims=3, dtype="fp64")
+    uid = SlabJob.unique_id()
+    with pytest.raises(_lib.StencilError):
+        SlabJob(spec, 32, 32, 20, devices=[gpu], rank=(2, 2, uid))  # rank out of range
+    with pytest.raises(_lib.StencilError):
+        SlabJob(spec, 32, 32, 20, devices=[gpu], rank=(1, 0, uid[:64]))  # not an RCCL id
+    with pytest.raises(ValueError):
+        SlabJob(spec, 32, 32, 20, devices=[gpu, gpu], rank=(1, 0, uid))  # one device per rank
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs 2 GPUs (RCCL refuses two ranks on one device)")
+def test_bench_rank_mode_two_processes(gpu):
+    """bench.py under torch.distributed.run, 2 ranks on 2 GPUs, through the
+    C-ABI rank-mode job: the JSON line and its bitwise check against the
+    global grid (runs only where >= 2 GPUs are visible)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29587", os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--n", "128", "--steps", "16", "--warmup", "4"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["multi_gpu_check"]["bitwise_equal"], line
+    assert "rank-mode" in line["config"]["parallelism"]
