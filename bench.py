@@ -402,8 +402,9 @@ def main():
                               "events around the face-signalled whole-slab launches of extra rounds after the timed "
                               "region" if slab.signalled else
                               "events around the interior launches of extra rounds after the timed region"),
-               workload_key=f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else
-               ("C3_rolling_4096" if rolling else f"{args.config}_slab_{count}"),
+               workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu" + (f"_slab_x{world}" if multi else ""))
+               if args.config == "C2" else
+               ("C3_rolling_4096" if rolling else f"{args.config}_slab_{count}" + (f"_x{world}" if multi else "")),
                local=local, check=(check if world > 1 else None), cpu=(world == 1 and not loop),
                extra_config={"rolling": rolling_info} if rolling else None,
                kernels_per_launch=(kernel_launches / max(1.0, args.steps / sweeps_per_launch)) if rolling else 1.0)
@@ -541,8 +542,8 @@ def main_rank_job(args, world, rank, local):
                "boundary + interior launches per round",
                launch_timing="hipEvents around rank 0's " + ("whole-slab face-signalled" if kt["signalled"] else
                                                              "interior") + " launches of extra rounds after the timed region",
-               workload_key=f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else
-               f"{args.config}_slab_{info['planes']}",
+               workload_key=f"3d7pt_fp64_{n}cube_per_gpu_slab_x{world}" if args.config == "C2" else
+               f"{args.config}_slab_{info['planes']}_x{world}",
                local=local, check=check, cpu=False)
     dist.destroy_process_group()
 
@@ -595,7 +596,8 @@ def main_slab_job(args):
            rounds="one face-signalled launch per round" if kt["signalled"] else "boundary + interior launches per round",
            launch_timing="hipEvents around slab 0's " + ("whole-slab face-signalled" if kt["signalled"] else "interior")
                          + " launches of extra rounds after the timed region",
-           workload_key=f"3d7pt_fp64_{n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz // n_gpus}",
+           workload_key=(f"3d7pt_fp64_{n}cube_per_gpu_slab_x{n_gpus}" if args.config == "C2" else
+                         f"{args.config}_slab_{gnz // n_gpus}_x{n_gpus}"),
            local=0, check=check, cpu=False)
 
 

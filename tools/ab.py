@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--grid", type=int, nargs=3, default=[512, 512, 512])
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--variant", action="append", default=[],
-                    help="NAME=VALUE[,NAME=VALUE]; STEPS=k overrides --steps for that variant")
+                    help="NAME=VALUE[,NAME=VALUE]; STEPS=k overrides --steps for that variant, "
+                         "INIT=random|reference its input grid (default random, seed 7)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--launches", type=int, default=5)
     args = ap.parse_args()
@@ -43,18 +44,23 @@ def main():
         for v2 in variants:
             for k in v2:
                 os.environ.pop(k, None)
-        os.environ.update({k: x for k, x in v.items() if k != "STEPS"})
+        os.environ.update({k: x for k, x in v.items() if k not in ("STEPS", "INIT")})
+        init = v.get("INIT", "random")
+        if init != state["init"]:  # the variant's input grid (a; b is overwritten)
+            e.reset(init, 7)
+            state["init"] = init
 
     def steps(v):
         return int(v.get("STEPS", args.steps))
 
+    state = {"init": "random"}
     refs = {}
     for vi, v in enumerate(variants):  # warm-up + check against the first variant of the same step count
         setenv(v)
         e.sweepk(e.a, e.b, 0, nz, steps(v))
         torch.cuda.synchronize()
         out = e.interior(e.b).clone()
-        k = steps(v)
+        k = (steps(v), state["init"])
         if k not in refs:
             refs[k] = (v, out)
         else:
