@@ -142,15 +142,14 @@ int iterate_tk_steps(const stencil_problem& p) {
 // TEMPORALK): K-step launches of kernels_boxk.hip, remainder as a pair / single
 // (STENCIL_BOX_STEPS=3|4 forces K, 2: pairs only).  K = 3 beat pairs
 // (profiles/r02e_ab_box_k3.log: 2048^2 x 256 fp64 717 vs 651 Gcell/s, fp32
-// 1242 vs 1182); K = 4 (strip 3 x 8) beats K = 3 for fp64 planes of 768^2
-// cells and more (768^2 x 512 792 vs 702, 1024^2 x 512 789 vs 704, 2048^2 x 256
-// 808 vs 686, 2048^3 861 vs 652) but not at 512^3 (733 vs 778) nor in fp32,
-// where its shape spills (882 vs 1506; profiles/r02u_ab_box_k4.log,
-// r02aa_ab_box_k4_threshold.log).  0 = not used.
+// 1242 vs 1182).  K = 4: since round 3's box order the strip kernel runs it
+// in 5 x 8 rows without spilling: 2048^2 x 256 fp64 1108 vs 743 (K = 3),
+// fp32 1997 vs 1538, 512^3 fp64 1096 vs 870 (profiles/r03/r03k_ab_box*.txt);
+// planes below 384^2 keep K = 3 (fewer, narrower tiles).  0 = not used.
 int iterate_box_steps(const stencil_problem& p) {
     if (!box27_supports(p)) return 0;
     if (!(p.kernel == STENCIL_KERNEL_TEMPORALK || (p.kernel == STENCIL_KERNEL_AUTO && iterate_fused(p)))) return 0;
-    const int steps = api_knob("STENCIL_BOX_STEPS", p.dtype == STENCIL_F64 && p.nx * p.ny >= int64_t(640) * 640 ? 4 : 3);
+    const int steps = api_knob("STENCIL_BOX_STEPS", p.nx * p.ny >= int64_t(384) * 384 ? 4 : 3);
     return steps == 3 || steps == 4 ? steps : 0;
 }
 

@@ -283,29 +283,29 @@ bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& 
                     const int64_t c = ((z + zr) * in.rows_with_boundary() + (y + r)) * sx + (x + r);
                     T sum = T(0);
                     if (options.box) {
-                        // separable partial sums (no reference code)
-                        const int rz = options.dims == 3 ? r : 0;
+                        // separable partial sums (no reference code):
+                        // 3D (P(-r) + .. + P(r)) - centre, 2D W + E
                         auto rowsum = [&](int64_t q) {
                             T a = src[q - r];
                             for (int dx = -r + 1; dx <= r; ++dx) a += src[q + dx];
                             return a;
                         };
-                        for (int dz = -rz; dz <= rz; ++dz) {
-                            const int64_t pl = c + dz * sxy;
-                            T term;
-                            if (dz != 0) {
-                                term = rowsum(pl - r * sx);
+                        if (options.dims == 3) {
+                            for (int dz = -r; dz <= r; ++dz) {
+                                const int64_t pl = c + dz * sxy;
+                                T term = rowsum(pl - r * sx);
                                 for (int dy = -r + 1; dy <= r; ++dy) term += rowsum(pl + dy * sx);
-                            } else {
-                                T w = rowsum(pl - r * sx);
-                                for (int dy = -r + 1; dy <= r; ++dy)
-                                    if (dy != 0) w += rowsum(pl + dy * sx);
-                                T e = src[pl - r];
-                                for (int dx = -r + 1; dx <= r; ++dx)
-                                    if (dx != 0) e += src[pl + dx];
-                                term = w + e;
+                                sum = dz == -r ? term : sum + term;
                             }
-                            sum = dz == -rz ? term : sum + term;
+                            sum = sum - src[c];
+                        } else {
+                            T w = rowsum(c - r * sx);
+                            for (int dy = -r + 1; dy <= r; ++dy)
+                                if (dy != 0) w += rowsum(c + dy * sx);
+                            T e = src[c - r];
+                            for (int dx = -r + 1; dx <= r; ++dx)
+                                if (dx != 0) e += src[c + dx];
+                            sum = w + e;
                         }
                     } else {
                         for (int k = r; k >= 1; --k) sum += src[c - k];       // left

@@ -4,22 +4,24 @@
 // Sum order (no reference code for the box; defined in DESIGN.md §3 and
 // restated by oracle/oracle_impl.inc):
 //     R(y')  = (in[x-1] + in[x]) + in[x+1]          row sum of row y'
-//     E      = in[x-1] + in[x+1]                    centre row without the centre
 //     P9(z') = (R(y-1) + R(y)) + R(y+1)              plane sum of plane z'
-//     C(z)   = (R(y-1) + R(y+1)) + E                 centre plane without the centre
-//     cell   = ((P9(z-1) + C(z)) + P9(z+1)) * avg
+//     cell   = (((P9(z-1) + P9(z)) + P9(z+1)) - in[z,y,x]) * avg
 // Row sums are shared by the three cells above / at / below a row, plane sums
-// by the cells below / above a plane: ~11 VALU operations per cell and stage
-// instead of the 26 dependent additions of a lexicographic order.
+// by the three cells below / at / above a plane: 8 VALU operations per cell
+// and stage (round 2 summed the centre plane without its centre,
+// ((P9(z-1) + C(z)) + P9(z+1)): 10, and the centre-row sum E = l + r live
+// beside every row sum -- the order change cut 236 -> 144 VGPRs at 3 x 8 rows,
+// K = 4) instead of the 26 dependent additions of a
+// lexicographic order.
 //
 // Pipeline (as the round-1 kernel: stage s lags stage s-1 by two planes).
 // When plane q of t_{s-1} is "in LDS", stage s
-//     finishes t_s(q-1) = A(q-1) + P9(q)            -> * avg
-//     continues        A(q)  = P9(q-1) + C(q)
+//     finishes t_s(q-1) = ((A(q-1) + P9(q)) - centre(q-1)) * avg
+//     continues        A(q)  = P9(q-1) + P9(q)
 // with A and P9 carried in registers from plane to plane.  What LDS holds of
 // plane q is only its row sums R (the rows y-1, y, y+1: three LDS reads); the
-// lane keeps the plane's values themselves (E from them by DPP lane shifts,
-// and the centre for the ghost cells of intermediate planes).  Per stage and
+// lane keeps the plane's values themselves (the centre, also the value of
+// the ghost cells of intermediate planes).  Per stage and
 // row a lane carries 4 vectors (centre of q and q-1, A, P9; the last stage 3),
 // so 8 waves x 4 rows fit 256 VGPRs.
 //
@@ -94,8 +96,8 @@ struct BKTile {
 // kernels_strip.hip): the last z-chunk of every tile marches DOWNWARD, so the
 // K planes of both faces are among the first stored, and the workgroup that
 // stores a face adds to sig[0] / sig[1] (release, then one agent-scope add).
-// Marching down, plane z's sum ((P9(z-1) + C(z)) + P9(z+1)) needs the NEWEST
-// plane sum first, so the down-march carries C(z) and the two previous plane
+// Marching down, plane z's sum ((P9(z-1) + P9(z)) + P9(z+1)) - centre needs the
+// NEWEST plane sum first, so the down-march carries the two previous plane
 // sums instead of the pre-added A: same additions, same order, bitwise equal.
 template <typename T, int V, int RY, int NW, int K, bool SIG = false>
 __global__ void __launch_bounds__(64 * NW)
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(64 * NW)
     VT vin[4][RY];
     VT H[K > 1 ? K - 1 : 1][2][RY];
     // per stage, carried from plane to plane: up-march A(q-1) and P9(q-1);
-    // down-march (REV) C(q-1), P9(q-1), P9(q-2) (march order)
+    // down-march (REV) P9(q-1), P9(q-2) (march order)
     VT A[K][RY], P9p[K][RY], P9q[REV ? K : 1][RY];
 #pragma unroll
     for (int k = 0; k < RY; ++k) {
@@ -231,20 +233,18 @@ __global__ void __launch_bounds__(64 * NW)
                 // plane q = p - 2s + 1 and q - 1 of t_{s-1}: s = 1 -> in(p-1), in(p-2)
                 const VT& cq = s == 1 ? vin[(S + 3) % 4][k] : H[s >= 2 ? s - 2 : 0][(S + 1) & 1][k];
                 const VT& cq1 = s == 1 ? vin[(S + 2) % 4][k] : H[s >= 2 ? s - 2 : 0][S & 1][k];
-                const VT E = row_sum(cq, false);
+                (void)cq;
                 VT o;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
                     const T p9 = (up[j] + own[j]) + dn[j];
-                    const T c = (up[j] + dn[j]) + E[j];
                     T fin;
-                    if constexpr (!REV) {
-                        fin = A[s - 1][k][j] + p9;  // (P9(q-2) + C(q-1)) + P9(q)
-                        A[s - 1][k][j] = P9p[s - 1][k][j] + c;
+                    if constexpr (!REV) {  // plane q-1: ((P9(q-2) + P9(q-1)) + P9(q)) - centre
+                        fin = (A[s - 1][k][j] + p9) - cq1[j];
+                        A[s - 1][k][j] = P9p[s - 1][k][j] + p9;
                         P9p[s - 1][k][j] = p9;
-                    } else {  // plane zr(q-1): (P9(zr(q)) + C(zr(q-1))) + P9(zr(q-2))
-                        fin = (p9 + A[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j];
-                        A[s - 1][k][j] = c;
+                    } else {  // plane zr(q-1): ((P9(zr(q)) + P9(zr(q-1))) + P9(zr(q-2))) - centre
+                        fin = ((p9 + P9p[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j]) - cq1[j];
                         P9q[REV ? s - 1 : 0][k][j] = P9p[s - 1][k][j];
                         P9p[s - 1][k][j] = p9;
                     }
@@ -446,22 +446,17 @@ __global__ void __launch_bounds__(64 * NW)
     // the whole region inside the grid in x and y (the fast path's condition)
     const bool xy_inner = fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
                           int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny;
-    // R = (l + c) + r and E = l + r of a row vector (x-neighbours by DPP)
-    auto sums = [&](const VT& v, VT& R, VT& E) {
+    // R = (l + c) + r of a row vector (x-neighbours by DPP)
+    auto rsum = [&](const VT& v) {
         const T wl = bdpp<kShr1>(v[V - 1]);
         const T er = bdpp<kShl1>(v[0]);
+        VT R;
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
             const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
-            const T e = l + r;
-            E[j] = e;
             R[j] = (l + v[j]) + r;
         }
-    };
-    auto rsum = [&](const VT& v) {
-        VT R, E;
-        sums(v, R, E);
         return R;
     };
     const int xl = lane * V;
@@ -483,7 +478,7 @@ __global__ void __launch_bounds__(64 * NW)
     };
 
     // in(m) in vin[(m - p0) % 4], t_s(m) in H[s-1][(m - p0) & 1] (read in
-    // place); per stage the carried A(q-1) / P9(q-1) (REV: C, P9(q-1), P9(q-2))
+    // place); per stage the carried A(q-1) / P9(q-1) (REV: P9(q-1), P9(q-2))
     const int p0 = za - K;
     VT vin[4][RY];
     VT H[K > 1 ? K - 1 : 1][2][RY];
@@ -519,26 +514,22 @@ __global__ void __launch_bounds__(64 * NW)
             auto cq = [&](int k) -> const VT& { return s == 1 ? vin[(S + 3) % 4][k] : H[s >= 2 ? s - 2 : 0][(S + 1) & 1][k]; };
             auto cq1 = [&](int k) -> const VT& { return s == 1 ? vin[(S + 2) % 4][k] : H[s >= 2 ? s - 2 : 0][S & 1][k]; };
             VT Rm = *reinterpret_cast<const VT*>(&L[PR][s - 1][wa][1][xl]);  // row above the strip
-            VT Rc, Ec;
-            sums(cq(0), Rc, Ec);
+            VT Rc = rsum(cq(0));
 #pragma unroll
             for (int k = 0; k < RY; ++k) {
-                VT Rn, En{};
-                if (k == RY - 1) Rn = *reinterpret_cast<const VT*>(&L[PR][s - 1][wb][0][xl]);  // row below
-                else sums(cq(k + 1 < RY ? k + 1 : k), Rn, En);
+                const VT Rn = k == RY - 1 ? *reinterpret_cast<const VT*>(&L[PR][s - 1][wb][0][xl])  // row below
+                                          : rsum(cq(k + 1 < RY ? k + 1 : k));
                 VT o;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
                     const T p9 = (Rm[j] + Rc[j]) + Rn[j];
-                    const T c = (Rm[j] + Rn[j]) + Ec[j];
                     T fin;
-                    if constexpr (!REV) {
-                        fin = A[s - 1][k][j] + p9;  // (P9(q-2) + C(q-1)) + P9(q)
-                        A[s - 1][k][j] = P9p[s - 1][k][j] + c;
+                    if constexpr (!REV) {  // plane q-1: ((P9(q-2) + P9(q-1)) + P9(q)) - centre, A = P9(q-2) + P9(q-1)
+                        fin = (A[s - 1][k][j] + p9) - cq1(k)[j];
+                        A[s - 1][k][j] = P9p[s - 1][k][j] + p9;
                         P9p[s - 1][k][j] = p9;
-                    } else {  // plane zr(q-1): (P9(zr(q)) + C(zr(q-1))) + P9(zr(q-2))
-                        fin = (p9 + A[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j];
-                        A[s - 1][k][j] = c;
+                    } else {  // plane zr(q-1): ((P9(zr(q)) + P9(zr(q-1))) + P9(zr(q-2))) - centre
+                        fin = ((p9 + P9p[s - 1][k][j]) + P9q[REV ? s - 1 : 0][k][j]) - cq1(k)[j];
                         P9q[REV ? s - 1 : 0][k][j] = P9p[s - 1][k][j];
                         P9p[s - 1][k][j] = p9;
                     }
@@ -565,7 +556,6 @@ __global__ void __launch_bounds__(64 * NW)
                 }
                 Rm = Rc;
                 Rc = Rn;
-                Ec = En;
             }
         };
         stage(std::integral_constant<int, K>{});
@@ -778,6 +768,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 2940208: return launch_bk<float, 4, 2, 8, 2, false, true>(l, in, out, begin, end, s);
             case 3920216: return launch_bk<float, 2, 2, 16, 3, false, true>(l, in, out, begin, end, s);
             case 1940408: return launch_bk<float, 4, 4, 8, 1, false, true>(l, in, out, begin, end, s);
+            case 3920608: return launch_bk<float, 2, 6, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 4920508: return launch_bk<float, 2, 5, 8, 4, false, true>(l, in, out, begin, end, s);
             default: break;
             }
         } else {
@@ -794,6 +786,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 2910216: return launch_bk<double, 1, 2, 16, 2, false, true>(l, in, out, begin, end, s);
             case 3910216: return launch_bk<double, 1, 2, 16, 3, false, true>(l, in, out, begin, end, s);
             case 1920408: return launch_bk<double, 2, 4, 8, 1, false, true>(l, in, out, begin, end, s);
+            case 3910608: return launch_bk<double, 1, 6, 8, 3, false, true>(l, in, out, begin, end, s);
+            case 4910508: return launch_bk<double, 1, 5, 8, 4, false, true>(l, in, out, begin, end, s);
             default: break;
             }
         }
@@ -860,9 +854,13 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         default: break;
         }
     }
-    if (steps == 4) {  // strip layout, 3 rows x 8 waves (4 rows spill)
-        if (l.prob.dtype == STENCIL_F32) return launch_bk<float, 2, 3, 8, 4, false, true>(l, in, out, begin, end, s);
-        return launch_bk<double, 1, 3, 8, 4, false, true>(l, in, out, begin, end, s);
+    if (steps == 4) {
+        // strip layout, 5 rows x 8 waves (40 rows for 32 output rows): fits
+        // since round 3's box order (fp64 238 VGPRs, fp32 249); 2048^2 x 256
+        // fp64 1108 vs 1057 (4 x 8) and 850 (3 x 8) Gcell/s, fp32 1997 vs
+        // 1895 / 1763; 512^3 fp64 1096 vs 979 / 762 (profiles/r03/r03k_ab_box*.txt)
+        if (l.prob.dtype == STENCIL_F32) return launch_bk<float, 2, 5, 8, 4, false, true>(l, in, out, begin, end, s);
+        return launch_bk<double, 1, 5, 8, 4, false, true>(l, in, out, begin, end, s);
     }
     return set_error(STENCIL_EINVAL, "box kernel steps must be 1..4 (got %d)", steps);
 }
@@ -879,6 +877,8 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
             switch (steps * 1000000 + cfg) {
             case 3920408: return launch_bk<float, 2, 4, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             case 3920308: return launch_bk<float, 2, 3, 8, 3, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4920408: return launch_bk<float, 2, 4, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4920508: return launch_bk<float, 2, 5, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             default: break;
             }
         } else {
@@ -889,6 +889,8 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
             case 4910308: return launch_bk<double, 1, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             case 4910212: return launch_bk<double, 1, 2, 12, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             case 4910216: return launch_bk<double, 1, 2, 16, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4910408: return launch_bk<double, 1, 4, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            case 4910508: return launch_bk<double, 1, 5, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
             default: break;
             }
         }
@@ -917,10 +919,10 @@ int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64
         default: break;
         }
     }
-    if (steps == 4) {  // strip layout, 3 rows x 8 waves (as launch_boxk)
+    if (steps == 4) {  // strip layout, 5 rows x 8 waves (as launch_boxk)
         if (l.prob.dtype == STENCIL_F32)
-            return launch_bk<float, 2, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-        return launch_bk<double, 1, 3, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+            return launch_bk<float, 2, 5, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        return launch_bk<double, 1, 5, 8, 4, true, true>(l, in, out, begin, end, s, sig, nsig, fsig);
     }
     return set_error(STENCIL_EINVAL, "face-signalled box sweeps: steps must be 2..4 (got %d)", steps);
 }

@@ -12,9 +12,9 @@
 //          stencil_dma.cpp:636-650 (r > 1) -- 0 + row window + column window
 //          - (centre + centre), then * avg
 //   BOX  : separable partial sums (no reference code; DESIGN.md §3,
-//          oracle/oracle_impl.inc): row sums R, plane sums P, the centre
-//          plane's other rows W and centre row E, S = P(-r)..P(-1) + (W + E)
-//          + P(1)..P(r), then * avg
+//          oracle/oracle_impl.inc): row sums R, plane sums P; 3D
+//          S = (P(-r) + .. + P(r)) - centre, 2D S = W + E (the centre row's
+//          other rows W, centre row E), then * avg
 // The library is compiled with -ffp-contract=off so no FMA changes rounding.
 #include "common.hpp"
 
@@ -27,30 +27,28 @@ __device__ __forceinline__ T cell(const T* __restrict__ c, int64_t row, int64_t 
     const int r = R > 0 ? R : rr;
     T sum = T(0);
     if constexpr (SHAPE == STENCIL_BOX) {
-        const int rz = DIMS == 3 ? r : 0;
         auto rowsum = [&](const T* q) {  // q -> the row's centre cell
             T a = q[-r];
             for (int dx = -r + 1; dx <= r; ++dx) a += q[dx];
             return a;
         };
-        for (int dz = -rz; dz <= rz; ++dz) {
-            const T* pl = c + dz * plane;
-            T term;
-            if (dz != 0) {
-                term = rowsum(pl - r * row);
+        if constexpr (DIMS == 3) {  // (P(-r) + ... + P(r)) - centre
+            for (int dz = -r; dz <= r; ++dz) {
+                const T* pl = c + dz * plane;
+                T term = rowsum(pl - r * row);
                 for (int dy = -r + 1; dy <= r; ++dy) term += rowsum(pl + dy * row);
-            } else {
-                T w = rowsum(pl - r * row);
-                for (int dy = -r + 1; dy <= r; ++dy)
-                    if (dy != 0) w += rowsum(pl + dy * row);
-                T e = pl[-r];
-                for (int dx = -r + 1; dx <= r; ++dx)
-                    if (dx != 0) e += pl[dx];
-                term = w + e;
+                sum = dz == -r ? term : sum + term;
             }
-            sum = dz == -rz ? term : sum + term;
+            return (sum - c[0]) * avg;
+        } else {  // W + E
+            T w = rowsum(c - r * row);
+            for (int dy = -r + 1; dy <= r; ++dy)
+                if (dy != 0) w += rowsum(c + dy * row);
+            T e = c[-r];
+            for (int dx = -r + 1; dx <= r; ++dx)
+                if (dx != 0) e += c[dx];
+            return (w + e) * avg;
         }
-        return sum * avg;
     } else if constexpr (ORDER == STENCIL_ORDER_DMA) {
         if (r == 1) return T(0.25) * (((c[-row] + c[-1]) + c[1]) + c[row]);
 #pragma unroll

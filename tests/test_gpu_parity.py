@@ -429,10 +429,10 @@ def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
     assert e.plan(8) == (3, 3)
 
 
-BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910216"],
-                            3: ["910408", "910308", "910312", "910212", "910216"],
+BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910508", "910216"],
+                            3: ["910408", "910308", "910312", "910212", "910216", "910608"],
                             2: ["910408", "910312", "910216"], 1: ["920408"]},
-                   "fp32": {4: ["920308", "920408"], 3: ["920408", "920312", "920216"],
+                   "fp32": {4: ["920308", "920408", "920508"], 3: ["920408", "920312", "920216", "920608"],
                             2: ["920408", "920312", "940208"], 1: ["940408"]}}
 
 
@@ -660,7 +660,7 @@ def test_full_size_baseline_configs(gpu, cfg):
 def test_box_packed_schedule(gpu, monkeypatch, pack):
     """The box's packed longest-first z-chunk schedule (few-tile fp64 grids,
     kernels_boxk.hip + kernels_strip.hip packed_schedule) at a shape where it
-    is used, 7 sweeps (two K = 3 launches + a single), bitwise against the
+    is used, 7 sweeps (a K = 4 launch, a pair and a single), bitwise against the
     oracle -- and with it switched off."""
     monkeypatch.setenv("STENCIL_BOXK_PACK", pack)
     nx, ny, nz = 400, 400, 400  # 112 tiles: 336 packed workgroups (STENCIL_TK_VERBOSE=1 prints the table size)
@@ -683,8 +683,8 @@ def test_benched_kernel_at_benched_shape(gpu, case):
       C4: 2048^2 x 512 fp64 (one GPU's slab of config 4), 8 sweeps = two
           K = 4 launches of equal z-chunks (too many tiles to pack);
       C5: 2048^2 x 256 fp64 box (one GPU's slab of config 5), 9 sweeps = two
-          K = 4 strip launches (fp64 planes >= 1024^2) + a single sweep;
-      box 512^3 fp64 (K = 3 strip 4 x 8) and 2048^2 x 64 fp32 (K = 3 strip)."""
+          K = 4 strip launches (5 x 8 rows) + a single sweep;
+      box 512^3 fp64 and 2048^2 x 64 fp32 (K = 4 strip 5 x 8: box planes >= 384^2)."""
     import torch
     from stencil_amd import _lib
     t2 = _lib.KERNEL_TEMPORAL2  # the box's fused family reports TEMPORAL2
@@ -692,8 +692,8 @@ def test_benched_kernel_at_benched_shape(gpu, case):
               "C3_4096sq_x32_fp32": ("star", "fp32", (4096, 4096, 32), 10, 5, (2, _lib.KERNEL_TEMPORALK), False),
               "C4_2048sq_x512_fp64": ("star", "fp64", (2048, 2048, 512), 8, 4, (2, _lib.KERNEL_TEMPORALK), False),
               "C5_2048sq_x256_box_fp64": ("box", "fp64", (2048, 2048, 256), 9, 4, (3, t2), None),
-              "box_512cube_fp64": ("box", "fp64", (512, 512, 512), 7, 3, (3, t2), None),
-              "box_2048sq_x64_fp32": ("box", "fp32", (2048, 2048, 64), 6, 3, (2, t2), None)}
+              "box_512cube_fp64": ("box", "fp64", (512, 512, 512), 9, 4, (3, t2), None),
+              "box_2048sq_x64_fp32": ("box", "fp32", (2048, 2048, 64), 8, 4, (2, t2), None)}
     shape, dtype, (nx, ny, nz), it, k, plan, packed = shapes[case]
     e = engine(gpu, 3, dtype, shape, 1, "naive", "auto", nx, ny, nz)
     assert e.fuse_steps == k

@@ -26,7 +26,7 @@ def spec(dtype, shape="star", r=1, kernel="auto"):
     ("fp32", "star", 1, (200, 90, 23)),   # K = 4 (small planes)
     ("fp32", "star", 1, (1024, 1024, 9)), # K = 5 (fp32 planes >= 1024^2: C3's kernel)
     ("fp64", "box", 1, (77, 40, 19)),     # K = 3
-    ("fp64", "box", 1, (700, 650, 11)),   # K = 4 (fp64 box planes >= 640^2)
+    ("fp64", "box", 1, (700, 650, 11)),   # K = 4 (box planes >= 384^2)
     ("fp64", "star", 2, (45, 23, 17)),    # single sweeps (direct kernel)
 ])
 def test_rolling_matches_oracle(gpu, dtype, shape, r, dims3):

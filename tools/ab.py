@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--variant", action="append", default=[],
                     help="NAME=VALUE[,NAME=VALUE]; STEPS=k overrides --steps for that variant, "
-                         "INIT=random|reference its input grid (default random, seed 7)")
+                         "INIT=random|reference its input grid (default random, seed 7), NOCHECK=1 skips its bitwise "
+                         "check (a variant with another sum order)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--launches", type=int, default=5)
     args = ap.parse_args()
@@ -44,7 +45,7 @@ def main():
         for v2 in variants:
             for k in v2:
                 os.environ.pop(k, None)
-        os.environ.update({k: x for k, x in v.items() if k not in ("STEPS", "INIT")})
+        os.environ.update({k: x for k, x in v.items() if k not in ("STEPS", "INIT", "NOCHECK")})
         init = v.get("INIT", "random")
         if init != state["init"]:  # the variant's input grid (a; b is overwritten)
             e.reset(init, 7)
@@ -61,7 +62,9 @@ def main():
         torch.cuda.synchronize()
         out = e.interior(e.b).clone()
         k = (steps(v), state["init"])
-        if k not in refs:
+        if v.get("NOCHECK"):
+            print(f"variant {v}: not checked (another sum order)", flush=True)
+        elif k not in refs:
             refs[k] = (v, out)
         else:
             it = torch.int64 if args.dtype == "fp64" else torch.int32
