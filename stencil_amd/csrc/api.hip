@@ -480,9 +480,9 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
     if (int rc = check_layout(l)) return rc;
     if (steps < 3 || steps > 5) return set_error(STENCIL_EINVAL, "steps must be 1..5 (got %d)", steps);
     const bool box = box27_supports(l->prob);
-    if (!temporal2_supports(l->prob) && !(box && steps <= 4))
+    if (!temporal2_supports(l->prob) && !(box && steps <= 5))
         return set_error(STENCIL_EUNSUPPORTED,
-                         "3- to 5-step fused sweeps cover the 3D r=1 naive 7-point star (3..5) and box (3, 4) only");
+                         "3- to 5-step fused sweeps cover the 3D r=1 naive 7-point star and box (3..5) only");
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");

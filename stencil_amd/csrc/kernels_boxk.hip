@@ -585,10 +585,11 @@ __global__ void __launch_bounds__(64 * NW)
             }
         }
         // stages K-1 .. 1
-        if constexpr (K >= 4) stage(std::integral_constant<int, (K >= 4 ? K - 1 : 1)>{});
+        if constexpr (K >= 5) stage(std::integral_constant<int, (K >= 5 ? 4 : 1)>{});
+        if constexpr (K >= 4) stage(std::integral_constant<int, (K >= 4 ? 3 : 1)>{});
         if constexpr (K >= 3) stage(std::integral_constant<int, (K >= 3 ? 2 : 1)>{});
         if constexpr (K >= 2) stage(std::integral_constant<int, 1>{});
-        static_assert(K >= 1 && K <= 4, "K = 1..4");
+        static_assert(K >= 1 && K <= 5, "K = 1..5");
         // stage 1's next input plane: in(p)
         *reinterpret_cast<VT*>(&L[PW][0][w][0][xl]) = rsum(vin[S][0]);
         *reinterpret_cast<VT*>(&L[PW][0][w][1][xl]) = rsum(vin[S][RY - 1]);
@@ -770,6 +771,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 1940408: return launch_bk<float, 4, 4, 8, 1, false, true>(l, in, out, begin, end, s);
             case 3920608: return launch_bk<float, 2, 6, 8, 3, false, true>(l, in, out, begin, end, s);
             case 4920508: return launch_bk<float, 2, 5, 8, 4, false, true>(l, in, out, begin, end, s);
+            case 5920408: return launch_bk<float, 2, 4, 8, 5, false, true>(l, in, out, begin, end, s);
+            case 5920508: return launch_bk<float, 2, 5, 8, 5, false, true>(l, in, out, begin, end, s);
             default: break;
             }
         } else {
@@ -788,6 +791,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
             case 1920408: return launch_bk<double, 2, 4, 8, 1, false, true>(l, in, out, begin, end, s);
             case 3910608: return launch_bk<double, 1, 6, 8, 3, false, true>(l, in, out, begin, end, s);
             case 4910508: return launch_bk<double, 1, 5, 8, 4, false, true>(l, in, out, begin, end, s);
+            case 5910408: return launch_bk<double, 1, 4, 8, 5, false, true>(l, in, out, begin, end, s);
+            case 5910508: return launch_bk<double, 1, 5, 8, 5, false, true>(l, in, out, begin, end, s);
             default: break;
             }
         }
@@ -862,7 +867,7 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         if (l.prob.dtype == STENCIL_F32) return launch_bk<float, 2, 5, 8, 4, false, true>(l, in, out, begin, end, s);
         return launch_bk<double, 1, 5, 8, 4, false, true>(l, in, out, begin, end, s);
     }
-    return set_error(STENCIL_EINVAL, "box kernel steps must be 1..4 (got %d)", steps);
+    return set_error(STENCIL_EINVAL, "box kernel steps must be 1..5 (got %d)", steps);
 }
 
 // Face-signalled box launches for multi-GPU slab rounds (stencil_sweepk_signal):
