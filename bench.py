@@ -49,8 +49,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH
 
 # BASELINE.json configs as bench workloads.  C2 (the default, the metric's
 # config) is weak-scaled: n^3 per GPU.  C3-C5 are the configs' global grids,
-# z-slab split over the ranks (strong scaling); they need as many GPUs as
-# their two grids need memory (C3: 2 x 275 GB, C4: 2 x 137 GB).
+# z-slab split over the ranks (strong scaling); at N = 1, C3 and C4 keep ONE
+# resident grid (two would need 2 x 275 GB / 2 x 137 GB).
 PRESETS = {
     "C2": dict(dtype="fp64", shape="star", grid=None, min_gpus=1,
                desc="BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU"),
@@ -58,7 +58,8 @@ PRESETS = {
     # since two grids are 2 x 279 GB
     "C3": dict(dtype="fp32", shape="star", grid=(4096, 4096, 4096), min_gpus=1,
                desc="BASELINE config 3: 3D 7-point fp32 Jacobi, 4096^3"),
-    "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=2,
+    # C4 on one GPU likewise (one 137 GB grid + a margin)
+    "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=1,
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
     "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
                desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, temporal blocking (4 sweeps per launch, "
@@ -260,10 +261,11 @@ def main():
     else:                    # strong scaling: the global grid split in z-slabs
         gnx, gny, gnz = pre["grid"]
         first, count = partition(gnz, world, rank)
-    # C3 on one GPU: two grids do not fit (2 x 279 GB); ONE resident grid plus
-    # a rolling margin of spare planes (stencil_rolling_*, bitwise the
-    # two-grid job), the margin as deep as the free HBM allows
-    rolling = args.config == "C3" and world == 1 and not loop
+    # C3 / C4 on one GPU: two grids do not fit (C3 2 x 279 GB) or leave no room
+    # (C4 2 x 138 GB); ONE resident grid plus a rolling margin of spare planes
+    # (stencil_rolling_*, bitwise the two-grid job), the margin as deep as the
+    # free HBM allows (at most 512 planes)
+    rolling = args.config in ("C3", "C4") and world == 1 and not loop
     spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
     multi = world > 1 or loop  # the slab round structure (exchange + two streams)
     extra = 0
@@ -280,7 +282,8 @@ def main():
         need = RollingGrid.bytes_needed(spec, gnx, gny, gnz, 8)
         shift = int(min(512, (free - need - (2 << 30)) // plane_b + 8))
         if shift < 16:
-            raise SystemExit(f"--config C3 on one GPU needs {need / 2**30:.0f} GiB + a margin; {free / 2**30:.0f} GiB free")
+            raise SystemExit(f"--config {args.config} on one GPU needs {need / 2**30:.0f} GiB + a margin; "
+                             f"{free / 2**30:.0f} GiB free")
         grid = RollingGrid(spec, gnx, gny, gnz, shift, device=local)
         grid.reset("reference")
         kname = "temporalk"
@@ -404,7 +407,8 @@ def main():
                               "events around the interior launches of extra rounds after the timed region"),
                workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu" + (f"_slab_x{world}" if multi else ""))
                if args.config == "C2" else
-               ("C3_rolling_4096" if rolling else f"{args.config}_slab_{count}" + (f"_x{world}" if multi else "")),
+               ("C3_rolling_4096" if rolling and args.config == "C3" else f"{args.config}_rolling" if rolling else
+                f"{args.config}_slab_{count}" + (f"_x{world}" if multi else "")),
                local=local, check=(check if world > 1 else None), cpu=(world == 1 and not loop),
                extra_config={"rolling": rolling_info} if rolling else None,
                kernels_per_launch=(kernel_launches / max(1.0, args.steps / sweeps_per_launch)) if rolling else 1.0)

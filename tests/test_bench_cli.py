@@ -38,8 +38,9 @@ def test_slab_job_shared_device_rehearsal():
         bench.slab_job_plan(args(gpus=2, exchange="host"), 8)
 
 
-def test_c3_runs_on_one_gpu():
+def test_c3_c4_run_on_one_gpu():
     assert bench.PRESETS["C3"]["min_gpus"] == 1  # one resident grid + a rolling margin
+    assert bench.PRESETS["C4"]["min_gpus"] == 1
 
 
 def test_bench_gpus_2_without_launcher_fails_clearly_without_gpus():

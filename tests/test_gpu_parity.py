@@ -431,13 +431,13 @@ def test_boxk_three_steps(gpu, monkeypatch, dtype, shape3, cfg, zchunk):
 
 BOX_STRIP_CFGS = {"fp64": {4: ["910308", "910408", "910508", "910216"],
                             3: ["910408", "910308", "910312", "910212", "910216", "910608"],
-                            2: ["910408", "910312", "910216"], 1: ["920408"]},
+                            2: ["910408", "910312", "910216"], 1: ["920408"], 5: ["910408"]},
                    "fp32": {4: ["920308", "920408", "920508"], 3: ["920408", "920312", "920216", "920608"],
-                            2: ["920408", "920312", "940208"], 1: ["940408"]}}
+                            2: ["920408", "920312", "940208"], 1: ["940408"], 5: ["920408"]}}
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("steps", [1, 2, 3, 4])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (7, 5, 3), (250, 119, 12), (64, 300, 40)])
 @pytest.mark.parametrize("zchunk", ["0", "5", "13"])
 def test_box_strip_shapes(gpu, monkeypatch, dtype, steps, shape3, zchunk):

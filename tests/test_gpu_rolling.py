@@ -82,44 +82,46 @@ def test_rolling_equals_two_grids_c3_planes(gpu):
     torch.cuda.empty_cache()
 
 
-def test_c3_full_size_on_one_gpu(gpu):
-    """BASELINE config 3 at its stated size, 4096^3 fp32 7-point, on ONE GPU
-    (two grids would need 2 x 279 GB): 10 sweeps of the rolling job from the
-    reference initial condition.  Size-independent checks against the
-    two-grid path on a 4096^2 x 64 grid: after t = 10 sweeps plane z depends
-    on planes z-10 .. z+10 only, so the deep grid's bottom 54 planes equal the
-    shallow grid's bottom 54, its top 54 the shallow grid's top 54, and every
-    plane in [10, nz - 10) the shallow grid's plane 32 -- bit for bit (whole
-    planes compared on the GPU); plus the bitwise x-mirror symmetry of the
-    reference initial condition."""
+@pytest.mark.parametrize("case", ["C3", "C4"])
+def test_full_size_on_one_gpu(gpu, case):
+    """BASELINE configs 3 and 4 at their stated sizes on ONE GPU -- C3 4096^3
+    fp32 (two grids would need 2 x 279 GB), C4 2048^2 x 4096 fp64 (2 x 138 GB)
+    -- `it` sweeps of the rolling job from the reference initial condition
+    (C3 10: two K = 5 passes; C4 8: two K = 4 passes).  Size-independent
+    checks against the two-grid path on an nx x ny x 64 grid: after t sweeps
+    plane z depends on planes z-t .. z+t only, so the deep grid's bottom 64-t
+    planes equal the shallow grid's bottom 64-t, its top 64-t the shallow
+    grid's top 64-t, and every plane in [t, nz - t) the shallow grid's plane
+    32 -- bit for bit (whole planes compared on the GPU); plus the bitwise
+    x-mirror symmetry of the reference initial condition."""
     import gc
     import torch
     from stencil_amd.engine import JacobiEngine, RollingGrid
     gc.collect()
     torch.cuda.empty_cache()  # earlier tests' cached blocks: this test needs the whole HBM
-    nx = ny = 4096
-    it = 10
-    sp = spec("fp32")
+    dtype, nx, ny, nz, it = {"C3": ("fp32", 4096, 4096, 4096, 10), "C4": ("fp64", 2048, 2048, 4096, 8)}[case]
+    sp = spec(dtype)
     e = JacobiEngine(sp, nx, ny, 64, device=gpu)
     e.reset()
     fin, _ = e.iterate(it)
-    ref = e.interior(fin).clone()  # 64 planes, 4.3 GB
+    ref = e.interior(fin).clone()  # 64 planes, 4.3 GB (C3) / 2.1 GB (C4)
     del e, fin
     torch.cuda.empty_cache()
-    nz = 4096
     free = torch.cuda.mem_get_info(gpu)[0]
     lay_plane = RollingGrid.bytes_needed(sp, nx, ny, 1, 64) - RollingGrid.bytes_needed(sp, nx, ny, 1, 63)
     grid_bytes = RollingGrid.bytes_needed(sp, nx, ny, nz, 6)
     shift = int(min(400, (free - grid_bytes - (2 << 30)) // lay_plane + 6))
     assert shift >= 40, f"free {free / 2**30:.1f} GiB leaves no room for the rolling margin"
     g = RollingGrid(sp, nx, ny, nz, shift, device=gpu)
+    assert g.sweeps_per_pass == it // 2
     g.reset()
     g.iterate(it)
     got = g.interior()
-    assert torch.equal(got[:54], ref[:54])
-    assert torch.equal(got[nz - 54:], ref[64 - 54:])
+    keep = 64 - it
+    assert torch.equal(got[:keep], ref[:keep])
+    assert torch.equal(got[nz - keep:], ref[64 - keep:])
     mid = ref[32]
-    for z in range(10, nz - 10, 1):
+    for z in range(it, nz - it, 1):
         assert torch.equal(got[z], mid), z
     assert torch.equal(got[100], torch.flip(got[100], dims=[1]))
     # values in [0, 1] (every plane of `got` is bitwise one of `ref`'s, checked above)
