@@ -157,9 +157,8 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
-    // R = (l + c) + r or E = l + r of a row vector v (x-neighbours from the
-    // adjacent lanes)
-    auto row_sum = [&](const VT& v, bool centre) {
+    // R = (l + c) + r of a row vector v (x-neighbours from the adjacent lanes)
+    auto row_sum = [&](const VT& v) {
         const T wl = bdpp<kShr1>(v[V - 1]);
         const T er = bdpp<kShl1>(v[0]);
         VT o;
@@ -167,7 +166,7 @@ __global__ void __launch_bounds__(64 * NW)
         for (int j = 0; j < V; ++j) {
             const T l = j == 0 ? wl : v[j == 0 ? 0 : j - 1];
             const T r = j == V - 1 ? er : v[j == V - 1 ? 0 : j + 1];
-            o[j] = centre ? (l + v[j]) + r : l + r;
+            o[j] = (l + v[j]) + r;
         }
         return o;
     };
@@ -230,10 +229,8 @@ __global__ void __launch_bounds__(64 * NW)
                 const VT up = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy - 1][xl]);
                 const VT own = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy][xl]);
                 const VT dn = *reinterpret_cast<const VT*>(&L[PR][s - 1][yy + 1][xl]);
-                // plane q = p - 2s + 1 and q - 1 of t_{s-1}: s = 1 -> in(p-1), in(p-2)
-                const VT& cq = s == 1 ? vin[(S + 3) % 4][k] : H[s >= 2 ? s - 2 : 0][(S + 1) & 1][k];
+                // plane q - 1 of t_{s-1} (the centre of the plane finished now): s = 1 -> in(p-2)
                 const VT& cq1 = s == 1 ? vin[(S + 2) % 4][k] : H[s >= 2 ? s - 2 : 0][S & 1][k];
-                (void)cq;
                 VT o;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
@@ -314,7 +311,7 @@ __global__ void __launch_bounds__(64 * NW)
                 // t_s(p-2s-2), was stage s+1's plane q-1, read above)
                 if (s > 0) H[s > 0 ? s - 1 : 0][S & 1][k] = res[s > 0 ? s - 1 : 0][k];
                 const VT& v = s == 0 ? vin[S][k] : H[s > 0 ? s - 1 : 0][S & 1][k];
-                *reinterpret_cast<VT*>(&L[PW][s][yy][xl]) = row_sum(v, true);
+                *reinterpret_cast<VT*>(&L[PW][s][yy][xl]) = row_sum(v);
             }
         }
         load_plane(vin[(S + 2) % 4], p + 2);  // the slot of in(p-2), read above
