@@ -10,8 +10,9 @@ JOBS ?= 8
 # the reference's.  Denormals are kept (no FTZ): diffusion fronts decay into
 # the denormal range in long runs.  -fno-slp-vectorize: the SLP
 # vectoriser pairs independent fp32 adds of different rows into v_pk_add_f32,
-# and in the fp32 one-cell-per-lane box shapes that code computes wrong
-# values (the same source without SLP is bitwise right); the
+# and in the fp32 one-cell-per-lane box shapes of the pre-round-3 box order
+# LLVM's GCN DPP Combine pass then miscompiles that code (DESIGN.md §9.2b:
+# opt-bisect pins it to that pass; without SLP it is bitwise right); the
 # kernels' own vector types still give packed math within a lane.  Measured
 # equal or faster everywhere (fp32 box +6 %, profiles/r03/r03f_slp_ab.txt).
 HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize \
