@@ -125,7 +125,7 @@ struct StripTile {
 // LDS serves as per-wave register space: 28 VGPRs per lane fewer at RY = 7,
 // for 7 ds_write_b64 + 28 ds_read_b64 per wave and step, which pays for one
 // more fused sweep (K = 5) at the same 7-row strips.
-template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, int FP = 1,
+template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true,
           bool HL = false>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(64 * NW)
     for (int i = 0; i < NS - 2; ++i) load_plane(vin[i], p0 + i);
 
 
-    auto stepb = [&](auto S_, int p, auto FAST_, bool fast_rt) {
+    auto stepb = [&](auto S_, int p, auto FAST_) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % LCM
         constexpr bool FAST = decltype(FAST_)::value;  // no ghost-cell selects this step
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
@@ -343,19 +343,7 @@ __global__ void __launch_bounds__(64 * NW)
                     sum += REV ? zp[j] : zm[j];
                     sum += REV ? zm[j] : zp[j];
                     o[j] = DIAG == 2 ? c[j] : sfma0(sum, avg);
-                    if (s < K && !FAST) {
-                        if constexpr (FP == 2) {
-                            // one step body: a wave-uniform branch skips the
-                            // select on interior steps (the empty asm keeps the
-                            // compiler from speculating it back into selects)
-                            if (!fast_rt) {
-                                asm volatile("");
-                                o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
-                            }
-                        } else {
-                            o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
-                        }
-                    }
+                    if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
                 }
                 // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
                 if constexpr (s >= 2) hset(s - 1, (S - s + 5) & 1, k, prev);
@@ -426,7 +414,7 @@ __global__ void __launch_bounds__(64 * NW)
         // step costs the fp32 / signalled shapes their register fit
         constexpr bool kFast = TK_FAST_PATH && FP && sizeof(T) == 8 && V == 1 && !SIG && DIAG == 0;
         if constexpr (!kFast) {
-            stepb(S_, p, std::false_type{}, false);
+            stepb(S_, p, std::false_type{});
             return;
         }
         bool all_in = xy_inner;
@@ -435,12 +423,8 @@ __global__ void __launch_bounds__(64 * NW)
             const int z = zr(p - s);
             all_in = all_in && z >= (halo_lo ? -(K - s) : 0) && z < (halo_hi ? nz + (K - s) : nz);
         }
-        if constexpr (FP == 2) {
-            stepb(S_, p, std::false_type{}, all_in);
-        } else {
-            if (all_in) stepb(S_, p, std::true_type{}, false);
-            else stepb(S_, p, std::false_type{}, false);
-        }
+        if (all_in) stepb(S_, p, std::true_type{});
+        else stepb(S_, p, std::false_type{});
     };
 
     const int plast = zb + K - 1;
@@ -461,7 +445,7 @@ __global__ void __launch_bounds__(64 * NW)
 int senv_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
-          int FP = 1, bool HL = false>
+          bool FP = true, bool HL = false>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
@@ -819,9 +803,6 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             // stage 1's history in LDS (HL): 8-row strips at K = 4
             case 810808: return launch_st<double, 1, 8, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             case 810708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
-            // the interior fast path as a wave-uniform branch around each select
-            // (one step body) instead of a second copy of the step
-            case 730708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, 2>(l, in, out, begin, end, s);
             // 9-row strips without the fast path: 72 rows for 64 output rows (512 = 8 x 64)
             case 820908: return launch_st<double, 1, 9, 8, 4, true, 0, false, 4, false, true>(l, in, out, begin, end, s);
             default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
