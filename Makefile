@@ -47,6 +47,11 @@ $(OBJ)/knobs_debug.o: stencil_amd/csrc/knobs.cpp
 	@mkdir -p $(OBJ)
 	$(CXX) -O2 -std=c++17 -fPIC -Wall -DSTENCIL_DEBUG_KNOBS -c $< -o $@
 
+# the max-ILP copy of the strip kernel (kernels_strip_ilp.hip includes kernels_strip.hip); the scheduler
+# flag goes to the device compilation only (the host x86 backend has no such scheduler)
+$(OBJ)/kernels_strip_ilp.o: stencil_amd/csrc/kernels_strip.hip
+$(OBJ)/kernels_strip_ilp.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-ilp
+
 $(OBJ)/kernels_boxk_probe_noslp.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPROBE_NOSLP -fno-slp-vectorize -c $< -o $@

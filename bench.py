@@ -73,7 +73,8 @@ PRESETS = {
 # Kernel family (bench name) -> the sources that define it, hashed into the
 # traffic table so a PMC figure measured on older kernel code is not reported.
 KERNEL_SOURCES = {
-    "temporalk": ("stencil_amd/csrc/kernels_strip.hip", "stencil_amd/csrc/kernels_temporalk.hip"),
+    "temporalk": ("stencil_amd/csrc/kernels_strip.hip", "stencil_amd/csrc/kernels_strip_ilp.hip",
+                  "stencil_amd/csrc/kernels_temporalk.hip"),
     "temporal2": ("stencil_amd/csrc/kernels_temporal.hip",),
     "zmarch": ("stencil_amd/csrc/kernels_zmarch.hip",),
     "direct": ("stencil_amd/csrc/kernels_direct.hip",),

@@ -135,6 +135,10 @@ int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t
                      int steps, hipStream_t s);
 int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                    int cfg, hipStream_t s);
+// kernels_strip_ilp.hip: the fp64 K = 4 and fp32 K = 5 default strip shapes built under the gcn-max-ilp
+// machine scheduler (launch_tkstrip routes the shapes measured faster that way)
+int launch_tkstrip_ilp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                       hipStream_t s);
 int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                           unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s);
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,

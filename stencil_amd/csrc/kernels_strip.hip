@@ -571,6 +571,17 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
 
 }  // namespace
 
+#ifdef STRIP_ILP_TU
+// kernels_strip_ilp.hip: the two default shapes measured faster when this file is compiled under LLVM's
+// gcn-max-ilp machine scheduler: the fp64 K = 4 strip on grids of at most 2 tiles per
+// CU slot (the packed schedule with its interior fast path: 512^3 +1.5 %) and the fp32 K = 5 strip (C3).
+int launch_tkstrip_ilp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                       hipStream_t s) {
+    if (l.prob.dtype == STENCIL_F64 && steps == 4) return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
+    if (l.prob.dtype == STENCIL_F32 && steps == 5) return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
+    return set_error(STENCIL_EINVAL, "no max-ILP strip shape for %d steps", steps);
+}
+#else
 // Makespan (in plane steps) of workgroups of the given plane counts on
 // `slots` one-workgroup CU slots: workgroup i goes to XCD i % 8 (the
 // dispatcher's round robin), and inside an XCD to the slot that frees first
@@ -749,6 +760,19 @@ int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<
 }
 
 
+// Whether launch_st would consider the packed schedule for this shape (a
+// single grid of at most 2 tiles per CU slot: packed_schedule's own test).
+template <typename T, int V, int RY, int NW, int K>
+static bool packed_regime(const stencil_layout& l) {
+    using Tl = StripTile<T, V, RY, NW, K, true>;
+    if (l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI)) return false;
+    const Geom g = geom_of(l);
+    const int64_t tiles = ((g.nx + Tl::TX - 1) / Tl::TX) * ((g.ny + Tl::TY - 1) / Tl::TY);
+    int slots = 0;
+    if (resident_slots(tkstrip_7pt<T, V, RY, NW, K, true>, 64 * NW, &slots) != STENCIL_OK) return false;
+    return tiles <= 2 * int64_t(slots);
+}
+
 // cfg = RY*100 + NW (rows per wave x waves); 0 = default shape.
 int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                    int cfg, hipStream_t s) {
@@ -792,6 +816,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
         if (steps == 4) {
             switch (cfg) {
             case 10808: return launch_st<double, 1, 8, 8, 4>(l, in, out, begin, end, s);
+            // the default shape from this file's build whatever the grid (AUTO takes the max-ILP build on
+            // packed-regime grids)
+            case 10708: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
             case 10608: return launch_st<double, 1, 6, 8, 4>(l, in, out, begin, end, s);
             case 404: return launch_st<double, 2, 4, 8, 4>(l, in, out, begin, end, s);
             case 510708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 5>(l, in, out, begin, end, s);
@@ -805,7 +832,10 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 810708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             // 9-row strips without the fast path: 72 rows for 64 output rows (512 = 8 x 64)
             case 820908: return launch_st<double, 1, 9, 8, 4, true, 0, false, 4, false, true>(l, in, out, begin, end, s);
-            default: return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
+            default:
+                // grids of at most 2 tiles per CU slot (packed schedule, fast path): the max-ILP build
+                if (packed_regime<double, 1, 7, 8, 4>(l)) return launch_tkstrip_ilp(l, in, out, begin, end, 4, s);
+                return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
             }
         }
     }
@@ -816,7 +846,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             // stage 1's history in LDS (HL): 6-row strips (226 VGPRs); 7 rows with one boundary buffer (254)
             case 820608: return launch_st<float, 2, 6, 8, 5, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             case 830708: return launch_st<float, 2, 7, 8, 5, false, 0, false, 4, true, true>(l, in, out, begin, end, s);
-            default: return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
+            // the default shape from this file's build (AUTO takes the max-ILP build)
+            case 20508: return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
+            default: return launch_tkstrip_ilp(l, in, out, begin, end, 5, s);
             }
         }
         switch (cfg) {
@@ -855,8 +887,11 @@ int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, in
     return set_error(STENCIL_EINVAL, "face-signalled sweeps: steps must be 3, 4 or 5 (got %d)", steps);
 }
 
+#endif  // STRIP_ILP_TU
+
 }  // namespace stencil
 
+#ifndef STRIP_ILP_TU
 // The packed-schedule model on the host, without a GPU (tests, tools): see
 // include/stencil_hip.h.
 int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk, int64_t* equal_steps,
@@ -874,3 +909,4 @@ int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots
     clear_error();
     return STENCIL_OK;
 }
+#endif  // STRIP_ILP_TU

@@ -280,7 +280,10 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
                                          ("4", "810808"), ("4", "810708"), ("5", "810708"), ("5", "810608"),
                                          ("4", "820908"), ("5", "830708"), ("5", "820608"),
                                          # the default shape without the interior fast path
-                                         ("4", "710708")])
+                                         ("4", "710708"),
+                                         # the default shapes from kernels_strip.hip's own build ("1": AUTO, the
+                                         # max-ILP build kernels_strip_ilp.hip on these small grids)
+                                         ("5", "20508")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])
