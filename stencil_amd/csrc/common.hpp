@@ -97,8 +97,14 @@ extern thread_local LaunchInfo* tl_dry_launch;
 // reports a table that would be used through *sched = kDrySchedule.
 enum { kPackUntested = 0, kPackPacked = 1, kPackEqual = 2 };
 extern const int* const kDrySchedule;
+// faces_out (face-signalled slab launches): each tile's first full chunk
+// starts at plane 0 marching up and its last full chunk ends at the top
+// marching down (planes < 0 in the table), the short remainder in between,
+// so both faces lie in chunks of the first dispatch round; no table unless a
+// tile has at least 3 chunks.
 int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr);
+                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr,
+                    bool faces_out = false);
 
 // The dispatcher model behind packed_schedule mispredicts some shapes badly
 // (measured: 504 x 512 x 512 fp64 packed 0.555 vs equal 0.450 ms per launch,

@@ -150,12 +150,14 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t tiles = int64_t(tiles_x) * tiles_y;
     int64_t lo, hi;
     bool rev = false;  // this workgroup's chunk marches down (SIG: the last chunk)
-    if (!SIG && sched) {
-        // packed schedule (STENCIL_TK_PACK, never on the face-signalled
-        // launches, whose code stays as it was): {tile, first plane, planes}
+    if (sched) {
+        // packed schedule (STENCIL_TK_PACK): {tile, first plane, planes}; on
+        // face-signalled launches planes < 0 marks the chunk that ends at the
+        // top face and marches down (packed_schedule's faces_out tables)
         const int* e = sched + 3 * int64_t(blockIdx.x);
         lo = int64_t(e[0]) * nzr + e[1];
-        hi = lo + e[2];
+        hi = lo + (e[2] < 0 ? -e[2] : e[2]);
+        rev = SIG && e[2] < 0;
     } else if (zchunk > 0) {
         int64_t t = blockIdx.x % tiles, c = blockIdx.x / tiles;
         if (!SIG && xcd_pw > 0) {
@@ -522,12 +524,18 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     // 1173 vs 1105 Gcell/s, tools/pack_ab.sh); not for slabs of a multi-GPU
     // job, whose one-round grid above is deliberate
     const int pack_mode = api_knob("STENCIL_TK_PACK", 1);
-    if (!SIG && zc > 0 && pack_mode && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 &&
-        !(l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI))) {
-        const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, slots, zc, s,
-                                       tl_dry_launch != nullptr, &sched, &nb, &verdict);
+    const bool halo = l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI);
+    if (zc > 0 && pack_mode && senv_int("STENCIL_TK_ZCHUNK", 0) <= 0 && (!halo || SIG) &&
+        (!SIG || knob("STENCIL_TK_PACK_SIG", 1))) {
+        // face-signalled slab launches: the model for one CU per XCD spared
+        // (the exchange's kernels run beside the launch), faces in the first
+        // round's chunks, and no timing trial (its extra launches would add to
+        // the face counters the exchange waits on): the model's choice
+        const int pslots = SIG ? slots - slots / 32 : slots;
+        const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, pslots, zc, s,
+                                       tl_dry_launch != nullptr, &sched, &nb, &verdict, SIG);
         if (rc != STENCIL_OK) return rc;
-        if (pack_mode != 1) verdict = nullptr;  // 2: the model's choice, unmeasured
+        if (pack_mode != 1 || SIG) verdict = nullptr;  // 2: the model's choice, unmeasured
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
@@ -653,8 +661,43 @@ const int* const kDrySchedule = reinterpret_cast<const int*>(uintptr_t(16));
 // The table lives in the memory of the device it was built on: the cache is
 // keyed by kernel and device ordinal and guarded (a process may drive several
 // GPUs from several threads: stencil_set_device is per thread).
+// Rewrite a packed table so that each tile's faces lie in full chunks: its
+// first full chunk at plane 0 (up), its last full chunk ending at nz
+// (planes < 0: down), the short remainder between them.  Same lengths per
+// tile, so the same dispatch order and makespan.  False (no table) when a
+// tile has fewer than 3 chunks.
+static bool faces_outward(std::vector<int>& tab, int64_t nz) {
+    std::map<int, std::vector<size_t>> by_tile;  // entry indices of each tile, in table order
+    int lc = 0;
+    for (size_t i = 0; i < tab.size(); i += 3) {
+        by_tile[tab[i]].push_back(i);
+        lc = std::max(lc, tab[i + 2]);
+    }
+    for (auto& [t, idx] : by_tile) {
+        if (idx.size() < 3) return false;
+        int64_t z = 0;
+        size_t full_seen = 0, full = 0;
+        for (size_t i : idx) full += tab[i + 2] == lc;
+        for (size_t i : idx) {  // full chunks bottom-up, the last one at the top; the remainder after the others
+            if (tab[i + 2] != lc) continue;
+            if (++full_seen == full) {
+                tab[i + 1] = int(nz - lc);
+                tab[i + 2] = -lc;
+            } else {
+                tab[i + 1] = int(z);
+                z += lc;
+            }
+        }
+        for (size_t i : idx)
+            if (tab[i + 2] > 0 && tab[i + 2] != lc) tab[i + 1] = int(z), z += tab[i + 2];
+        if (z != nz - lc) return false;  // the lengths do not tile the range as expected
+    }
+    return true;
+}
+
 int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
-                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict) {
+                    hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict,
+                    bool faces_out) {
     // Only grids of few tiles: with more than 2 tiles per slot the equal
     // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
     // Gcell/s), and the search would cost host time at the first launch.
@@ -680,6 +723,7 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
         int64_t base = 0, best = 0;
         pack_search(tiles, nz, fill, slots, zc, force_lc, &best_tab, &base, &best);
         hit = cache.try_emplace(key).first;
+        if (faces_out && !best_tab.empty() && !faces_outward(best_tab, nz)) best_tab.clear();
         if (!best_tab.empty() && (best * 50 < base * 49 || force_lc > 0)) {
             hit->second.workgroups = int64_t(best_tab.size() / 3);
             hit->second.host = std::move(best_tab);

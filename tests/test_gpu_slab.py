@@ -197,6 +197,37 @@ def test_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, fla
     assert sig[0].item() == nsig and sig[1].item() == nsig and sig[2].item() == 0 and nsig > 0
 
 
+@pytest.mark.parametrize("flags", [0, 3])
+@pytest.mark.parametrize("pack_sig", ["1", "0"])
+def test_sweepk_signal_packed_schedule(gpu, monkeypatch, capfd, flags, pack_sig):
+    """Face-signalled launches on a grid of few tiles take the packed schedule
+    with the faces outward (packed_schedule faces_out: each tile's first full
+    chunk at plane 0 marching up, its last one ending at the top marching
+    down, the short remainder between): bitwise stencil_sweepk, one counter
+    add per tile and face, at the benched 512^3 fp64 shape (110 tiles x 3
+    chunks); STENCIL_TK_PACK_SIG=0 (debug) keeps the equal one-round chunks."""
+    monkeypatch.setenv("STENCIL_TK_VERBOSE", "1")
+    monkeypatch.setenv("STENCIL_TK_PACK_SIG", pack_sig)
+    nx = ny = nz = 512
+    e = JacobiEngine(StencilSpec(dims=3, dtype="fp64", halo=4), nx, ny, nz, device=gpu, flags=flags)
+    e.reset("random", 13)
+    ref = torch.empty_like(e.b)
+    ref.copy_(e.b)
+    e.sweepk(e.a, ref, 0, nz, 4)
+    torch.cuda.synchronize()
+    capfd.readouterr()
+    sig = torch.zeros(4, dtype=torch.int32, device=e.a.device)
+    for launch in range(3):  # the counters run on over launches
+        nsig = e.sweepk_signal(e.a, e.b, 0, nz, 4, sig)
+        e.wait_counters(sig, nsig * (launch + 1), nsig * (launch + 1))
+        torch.cuda.synchronize()
+        assert torch.equal(e.b.view(torch.int64), ref.view(torch.int64)), launch
+    err = capfd.readouterr().err
+    assert sig[0].item() == 3 * nsig and sig[1].item() == 3 * nsig and sig[2].item() == 0 and nsig == 110
+    # the launch line (STENCIL_TK_VERBOSE) gives the grid: 110 tiles x {230, 230, 52} planes when packed
+    assert ("tiles 10x11, zchunk" in err) and (("330 workgroups" in err) == (pack_sig == "1")), err
+
+
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
 @pytest.mark.parametrize("steps", [2, 3, 4])
 @pytest.mark.parametrize("zchunk", ["0", "5", "9", "40"])
