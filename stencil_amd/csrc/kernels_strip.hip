@@ -796,10 +796,16 @@ int pick_schedule(std::atomic<int>* verdict, hipStream_t s, const std::function<
         if (e) (void)hipEventDestroy(e);
     if (err != hipSuccess)
         return set_error(STENCIL_EHIP, "schedule trial failed: %s", hipGetErrorString(err));
-    verdict->store(best[0] < best[1] ? kPackPacked : kPackEqual);
+    // The model predicted packing (a table exists only for a predicted gain of
+    // 2 % or more): keep it unless the trial finds it clearly slower (3 %),
+    // so noisy timings -- a profiler's counter passes, a busy GPU -- do not
+    // flip the choice between processes; the mispredictions measured were
+    // 7-20 %
+    const bool packed = best[0] <= best[1] * 1.03f;
+    verdict->store(packed ? kPackPacked : kPackEqual);
     if (senv_int("STENCIL_TK_VERBOSE", 0))
         std::fprintf(stderr, "schedule trial: packed %.4f ms, equal chunks %.4f ms -> %s\n", best[0], best[1],
-                     best[0] < best[1] ? "packed" : "equal chunks");
+                     packed ? "packed" : "equal chunks");
     return STENCIL_OK;
 }
 
