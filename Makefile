@@ -54,6 +54,9 @@ $(OBJ)/kernels_strip_ilp.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-il
 # the 2D kernels (tb2ds / tb2d / tb2d1) under the same scheduler: C1 fp64 +1.4 %, fp32 +2.3 %, the rest within
 # +-1.3 % (profiles/r03/r03am_*, r03an_*)
 $(OBJ)/kernels_tb2d.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-ilp
+# the box kernels without the scheduler's unclustered high-register-pressure stage: C5 (2048^3 fp64) +1.3 %,
+# fp32 512^3 +1.8 %, other box shapes within 1 % (profiles/r03/r03ap_*, r03aq_*)
+$(OBJ)/kernels_boxk.o: HIPFLAGS += -Xarch_device -mllvm=-amdgpu-disable-unclustered-high-rp-reschedule
 
 $(OBJ)/kernels_boxk_probe_noslp.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd/csrc/kernels_boxk.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
 	@mkdir -p $(OBJ)
