@@ -28,24 +28,29 @@ LIB_DBG := stencil_amd/libstencil_hip_debug.so
 CLI := build/bin/stencil_main
 SRCS := $(wildcard stencil_amd/csrc/*.hip)
 OBJ ?= build/obj
-# kernels_boxk_probe.hip is built twice: with and without SLP vectorisation
-OBJS := $(patsubst stencil_amd/csrc/%.hip,$(OBJ)/%.o,$(SRCS)) $(OBJ)/kernels_boxk_probe_noslp.o
+# kernels_boxk_probe.hip (a code-generation probe) is built twice, with and without SLP
+# vectorisation, and linked into the debug library only; the product links knobs.cpp's stubs instead
+PROBE_OBJS := $(OBJ)/kernels_boxk_probe.o $(OBJ)/kernels_boxk_probe_noslp.o
+OBJS := $(filter-out $(PROBE_OBJS),$(patsubst stencil_amd/csrc/%.hip,$(OBJ)/%.o,$(SRCS)))
 HOST_SRCS := $(wildcard stencil_amd/csrc/host/*.cpp)
 HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
 
-all: $(LIB) $(LIB_DBG) $(CLI) oracle
+# test infrastructure: slab_core.hpp's round logic on a CPU fake device (sweeps by the oracle)
+FAKE := tests/cpu_slab/libslab_fake.so
+
+all: $(LIB) $(LIB_DBG) $(CLI) oracle $(FAKE)
 
 $(OBJ)/%.o: stencil_amd/csrc/%.hip $(wildcard stencil_amd/csrc/*.hpp) include/stencil_hip.h
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJ)/knobs.o: stencil_amd/csrc/knobs.cpp
+$(OBJ)/knobs.o: stencil_amd/csrc/knobs.cpp stencil_amd/csrc/common.hpp include/stencil_hip.h
 	@mkdir -p $(OBJ)
-	$(CXX) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJ)/knobs_debug.o: stencil_amd/csrc/knobs.cpp
+$(OBJ)/knobs_debug.o: stencil_amd/csrc/knobs.cpp stencil_amd/csrc/common.hpp include/stencil_hip.h
 	@mkdir -p $(OBJ)
-	$(CXX) -O2 -std=c++17 -fPIC -Wall -DSTENCIL_DEBUG_KNOBS -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DSTENCIL_DEBUG_KNOBS -c $< -o $@
 
 # the max-ILP copy of the strip kernel (kernels_strip_ilp.hip includes kernels_strip.hip); the scheduler
 # flag goes to the device compilation only (the host x86 backend has no such scheduler)
@@ -69,8 +74,8 @@ $(OBJ)/kernels_boxk_probe.o: stencil_amd/csrc/kernels_boxk_probe.hip stencil_amd
 $(LIB): $(OBJS) $(OBJ)/knobs.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(OBJ)/knobs.o
 
-$(LIB_DBG): $(OBJS) $(OBJ)/knobs_debug.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(OBJ)/knobs_debug.o
+$(LIB_DBG): $(OBJS) $(PROBE_OBJS) $(OBJ)/knobs_debug.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) $(PROBE_OBJS) $(OBJ)/knobs_debug.o
 
 $(CLI): $(HOST_SRCS) $(HOST_HDRS) $(LIB) include/stencil_hip.h
 	@mkdir -p build/bin
@@ -80,8 +85,15 @@ oracle:
 	$(MAKE) -C oracle
 	bash oracle/ref/build.sh
 
+oracle/liboracle.so: oracle/oracle.c oracle/oracle_impl.inc oracle/oracle.h
+	$(MAKE) -C oracle
+
+$(FAKE): tests/cpu_slab/fake_dev.cpp stencil_amd/csrc/slab_core.hpp stencil_amd/csrc/errors.hpp include/stencil_hip.h oracle/liboracle.so
+	$(CXX) $(CXXFLAGS) -fPIC -shared -pthread -Istencil_amd/csrc -Ioracle -o $@ $< -Loracle -loracle \
+	    -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 clean:
-	rm -rf build $(LIB) $(LIB_DBG)
+	rm -rf build $(LIB) $(LIB_DBG) $(FAKE)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -117,7 +117,25 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
                     help="N>1: skip the bitwise check against the global grid run as one grid on rank 0")
-    return ap.parse_args()
+    ap.add_argument("--allow-debug-library", action="store_true",
+                    help="bench even when an experiment knob (a STENCIL_* variable the product ignores) is set, "
+                         "i.e. on libstencil_hip_debug.so; the JSON line names the library and the knobs either way")
+    args = ap.parse_args()
+    from stencil_amd import _lib
+    if _lib.debug_knobs_requested() and not args.allow_debug_library:
+        knobs = sorted(k for k in os.environ if k.startswith("STENCIL_") and k not in _lib.API_KNOBS)
+        raise SystemExit(f"experiment knobs set ({', '.join(knobs)}): this would bench libstencil_hip_debug.so; "
+                         "unset them or pass --allow-debug-library")
+    return args
+
+
+def library_info() -> dict:
+    """Which build of the HIP library produced the line, and every STENCIL_*
+    variable set in the environment (documented knobs included)."""
+    from stencil_amd import _lib
+    lib = _lib.load()
+    return {"library": os.path.basename(_lib.DEBUG_LIB_PATH if lib.stencil_debug_knobs() else _lib.LIB_PATH),
+            "stencil_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("STENCIL_")}}
 
 
 def host_threads() -> int:
@@ -393,10 +411,11 @@ def main():
         elif loop:
             parallelism = ("1 GPU rehearsing an interior rank (periodic halo, two streams, " +
                            ("device copies)" if args.exchange == "loopback" else "RCCL send/recv to self)"))
+        elif world == 1:
+            parallelism = "1 GPU, one process, the whole grid (no decomposition)"
         else:
             parallelism = f"z-slab x{world}, one process per GPU (torch.distributed.run)" + (
-                "" if not multi else ", RCCL halo P2P overlapped" if args.exchange == "nccl"
-                else ", host-staged gloo halo (rehearsal)")
+                ", RCCL halo P2P overlapped" if args.exchange == "nccl" else ", host-staged gloo halo (rehearsal)")
         report(args, pre, spec, kname, (gnx, gny, gnz), world, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
                kernel_launches, parallelism,
                rounds=(None if not multi else "one face-signalled launch per round" if slab.signalled else
@@ -651,6 +670,7 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
             "parallelism": parallelism,
             "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
             "rounds": rounds,
+            **library_info(),
         },
         "roofline": {
             "bound": "hbm",

@@ -321,13 +321,25 @@ int stencil_copy_bandwidth(void* dst, const void* src, int64_t bytes, int reps, 
  * copies (hipMemcpyPeerAsync; slabs may share a GPU).  PERIODIC joins the
  * two z ends into a ring (a rehearsal mode: one slab exchanges with itself). */
 enum { STENCIL_EXCHANGE_RCCL = 0, STENCIL_EXCHANGE_COPY = 1 };
-enum { STENCIL_SLAB_PERIODIC = 1 };
+/* PERIODIC: the z ends form a ring.  ROLLING: each slab keeps ONE resident
+ * grid plus a margin of spare planes instead of two grids (the scheme of
+ * stencil_rolling_*, per slab): a round is a pass of ceil(n / S) z-range
+ * launches (S = margin - K*radius), then the exchange -- for slabs whose two
+ * grids do not fit one GPU, e.g. the north star's 4096^3 fp64 on 2 GPUs (one
+ * 278 GB grid each).  Bitwise the two-grid job; no face-signalled rounds. */
+enum { STENCIL_SLAB_PERIODIC = 1, STENCIL_SLAB_ROLLING = 2 };
 typedef struct stencil_slab_job stencil_slab_job;
 
 /* global: a 3D problem with halo = 0 and flags = 0; devices: ngpus ordinals
  * (NULL = 0 .. ngpus-1).  Every slab must own at least K planes. */
 int stencil_slab_create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange,
                         int32_t flags, stencil_slab_job** job);
+/* The same with the rolling margin: margin_planes > 0 spare planes per slab
+ * (at least K*radius + 1), 0 = as deep as each device's free memory allows
+ * beside its grid (less a 4 GiB reserve for RCCL), at most 512.  Ignored
+ * without STENCIL_SLAB_ROLLING. */
+int stencil_slab_create2(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange,
+                         int32_t flags, int64_t margin_planes, stencil_slab_job** job);
 /* Rank mode: one process per GPU, as the reference's MPI-style launch and
  * torch.distributed.run give it.  Rank 0 makes an RCCL id
  * (stencil_slab_unique_id, STENCIL_SLAB_ID_BYTES bytes) and hands it to every
@@ -344,9 +356,15 @@ enum { STENCIL_SLAB_ID_BYTES = 128 };
 int stencil_slab_unique_id(void* id, int64_t bytes);
 int stencil_slab_create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int32_t device,
                              const void* id, int64_t id_bytes, int32_t flags, stencil_slab_job** job);
+int stencil_slab_create_rank2(const stencil_problem* global, int32_t nranks, int32_t rank, int32_t device,
+                              const void* id, int64_t id_bytes, int32_t flags, int64_t margin_planes,
+                              stencil_slab_job** job);
 int stencil_slab_destroy(stencil_slab_job* job);
 int stencil_slab_info(const stencil_slab_job* job, int32_t slab, int64_t* first_plane, int64_t* planes,
                       int32_t* device, int32_t* sweeps_per_round);
+/* Rolling slabs: the margin (0: two grids per slab) and the most z-range
+ * launches one pass makes on a slab of this process. */
+int stencil_slab_rolling_info(const stencil_slab_job* job, int64_t* margin_planes, int64_t* launches_per_pass);
 /* Initial condition of the global grid (global linear indices for the random
  * interior, as stencil_fill_initial on one grid), halos exchanged. */
 int stencil_slab_fill_initial(stencil_slab_job* job, int32_t init_kind, uint64_t seed);
@@ -362,10 +380,12 @@ int stencil_slab_run(stencil_slab_job* job, uint32_t iterations, float* elapsed_
 int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
 /* Kernel timing for roofline figures: with timing on, every round records
  * hipEvents around slab 0's compute launch (the whole slab in face-signalled
- * rounds, else its interior launch) on that launch's stream.  kernel_time
- * synchronises and returns the summed device time, the launches timed, the
- * interior cells one timed launch covers and whether rounds are signalled.
- * Enabling (or disabling) drops earlier records. */
+ * rounds, its interior launch in boundary + interior rounds, the pass's
+ * z-range launches in rolling rounds) on that launch's stream.  kernel_time
+ * synchronises and returns the summed device time, the spans timed, the
+ * interior cells one span covers and the round form (0 boundary + interior,
+ * 1 face-signalled, 2 rolling).  Enabling (or disabling) drops earlier
+ * records. */
 int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
 int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,
                              int32_t* signalled);

@@ -26,7 +26,7 @@ KERNEL_AUTO, KERNEL_DIRECT, KERNEL_ZMARCH, KERNEL_TEMPORAL2, KERNEL_TEMPORALK, K
 INIT_REFERENCE, INIT_RANDOM = 0, 1
 HALO_LO, HALO_HI = 1, 2
 EXCHANGE_RCCL, EXCHANGE_COPY = 0, 1
-SLAB_PERIODIC = 1
+SLAB_PERIODIC, SLAB_ROLLING = 1, 2
 SLAB_ID_BYTES = 128
 
 KERNEL_NAMES = {"auto": KERNEL_AUTO, "direct": KERNEL_DIRECT, "zmarch": KERNEL_ZMARCH, "temporal2": KERNEL_TEMPORAL2,
@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
     "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
     "stencil_slab_kernel_timing", "stencil_slab_kernel_time", "stencil_slab_unique_id", "stencil_slab_create_rank",
+    "stencil_slab_create2", "stencil_slab_create_rank2", "stencil_slab_rolling_info",
 )
 
 
@@ -102,8 +103,24 @@ def load(debug: bool | None = None) -> ctypes.CDLL:
             f"{path} is missing: the HIP extension has not been built "
             "(run `make` or `python -c 'import __graft_entry__ as g; g.build()'`)")
     lib = ctypes.CDLL(path)
+    for name, (res, args) in signatures().items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    for name in ("stencil_iterate_dma", "stencil_iterate_dma_static_unroll",
+                 "stencil_iterate_dma_slave_pack", "stencil_iterate_rma"):
+        fn = getattr(lib, name)
+        fn.restype = None
+        fn.argtypes = [POINTER(Arguments)]
+    _libs[debug] = lib
+    return lib
+
+
+def signatures() -> dict:
+    """(restype, argtypes) of every C-ABI function but the four reference
+    entry points (tests/cpu_slab/binding.py reuses the stencil_slab_* ones)."""
     P, L = POINTER(Problem), POINTER(Layout)
-    sig = {
+    return {
         "stencil_strerror": (c_char_p, [c_int]),
         "stencil_last_error_message": (c_char_p, []),
         "stencil_last_error": (c_int, []),
@@ -149,6 +166,11 @@ def load(debug: bool | None = None) -> ctypes.CDLL:
         "stencil_slab_unique_id": (c_int, [c_void_p, c_int64]),
         "stencil_slab_create_rank": (c_int, [POINTER(Problem), c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
                                              POINTER(c_void_p)]),
+        "stencil_slab_create2": (c_int, [POINTER(Problem), c_int32, POINTER(c_int32), c_int32, c_int32, c_int64,
+                                         POINTER(c_void_p)]),
+        "stencil_slab_create_rank2": (c_int, [POINTER(Problem), c_int32, c_int32, c_int32, c_void_p, c_int64, c_int32,
+                                              c_int64, POINTER(c_void_p)]),
+        "stencil_slab_rolling_info": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),
         "stencil_slab_info": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32),
                                       POINTER(c_int32)]),
         "stencil_slab_fill_initial": (c_int, [c_void_p, c_int32, c_uint64]),
@@ -160,17 +182,6 @@ def load(debug: bool | None = None) -> ctypes.CDLL:
         "stencil_slab_kernel_time": (c_int, [c_void_p, POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
                                              POINTER(c_int32)]),
     }
-    for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-    for name in ("stencil_iterate_dma", "stencil_iterate_dma_static_unroll",
-                 "stencil_iterate_dma_slave_pack", "stencil_iterate_rma"):
-        fn = getattr(lib, name)
-        fn.restype = None
-        fn.argtypes = [POINTER(Arguments)]
-    _libs[debug] = lib
-    return lib
 
 
 def check(rc: int, where: str, lib: ctypes.CDLL | None = None) -> None:

@@ -480,9 +480,13 @@ int stencil_sweepk(const stencil_layout* l, const void* in, void* out, int64_t b
     if (int rc = check_layout(l)) return rc;
     if (steps < 3 || steps > 5) return set_error(STENCIL_EINVAL, "steps must be 1..5 (got %d)", steps);
     const bool box = box27_supports(l->prob);
-    if (!temporal2_supports(l->prob) && !(box && steps <= 5))
+    // the box's K = 5 strip shapes are debug configurations only (DESIGN.md
+    // §9.2e: they lose to K = 4); the product library has no K = 5 box launch
+    const int box_max = stencil_debug_knobs() ? 5 : 4;
+    if (!temporal2_supports(l->prob) && !(box && steps <= box_max))
         return set_error(STENCIL_EUNSUPPORTED,
-                         "3- to 5-step fused sweeps cover the 3D r=1 naive 7-point star and box (3..5) only");
+                         "3- to 5-step fused sweeps cover the 3D r=1 naive 7-point star (3..5) and box (3..%d) only",
+                         box_max);
     if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
         return set_error(STENCIL_EINVAL, "sweep range out of bounds");
     if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <functional>
 
+#include "errors.hpp"
 #include "stencil_hip.h"
 
 namespace stencil {
@@ -26,11 +27,6 @@ struct Geom {
 inline Geom geom_of(const stencil_layout& l) {
     return Geom{l.prob.nx, l.prob.ny, l.prob.nz, l.row, l.plane, l.origin};
 }
-
-// Record an error for stencil_last_error_message(); returns `code`.
-int set_error(int code, const char* fmt, ...);
-// Clear the per-thread error state (success).
-void clear_error();
 
 // Workgroup slots of `kern` (launched with `threads` threads) on the CURRENT
 // device: CUs x resident workgroups per CU (one_per_cu: CUs only).  Cached

@@ -864,7 +864,8 @@ int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begi
         if (l.prob.dtype == STENCIL_F32) return launch_bk<float, 2, 5, 8, 4, false, true>(l, in, out, begin, end, s);
         return launch_bk<double, 1, 5, 8, 4, false, true>(l, in, out, begin, end, s);
     }
-    return set_error(STENCIL_EINVAL, "box kernel steps must be 1..5 (got %d)", steps);
+    return set_error(STENCIL_EINVAL, "box kernel steps must be 1..4 (got %d; K = 5 shapes are debug configurations)",
+                     steps);
 }
 
 // Face-signalled box launches for multi-GPU slab rounds (stencil_sweepk_signal):

@@ -712,7 +712,7 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
     static std::mutex mu;
     // map nodes never move: the verdict's address stays valid for the process
     static std::map<std::tuple<const void*, int, int64_t, int64_t, int, int, int>, Entry> cache;
-    std::lock_guard<std::mutex> lock(mu);
+    std::unique_lock<std::mutex> lock(mu);
     // STENCIL_TK_PACK_LC (experiments): chunks of exactly this many planes,
     // used whatever the model says
     const int force_lc = senv_int("STENCIL_TK_PACK_LC", 0);
@@ -748,16 +748,28 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
             cap = hipStreamCaptureStatusActive;
         }
         if (cap != hipStreamCaptureStatusNone) return STENCIL_OK;  // no allocation inside a capture: equal chunks
+        // Upload on a private stream of the caller's device, outside the
+        // lock: the host waits for this copy only -- not for the work queued
+        // on `s` (a slab round's counter wait and exchange) -- and other
+        // threads / devices are not held behind it.  The entry's host table
+        // never changes once built (map nodes do not move).
+        const std::vector<int>& host = e.host;
+        lock.unlock();
         int* d = nullptr;
-        if (hipMalloc(&d, e.host.size() * sizeof(int)) != hipSuccess ||
-            hipMemcpyAsync(d, e.host.data(), e.host.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess ||
-            // ordered before this launch on `s`; the wait (once per shape) also
-            // orders it before launches the caller puts on other streams
-            hipStreamSynchronize(s) != hipSuccess) {
+        hipStream_t up = nullptr;
+        hipError_t err = hipMalloc(&d, host.size() * sizeof(int));
+        if (err == hipSuccess) err = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
+        if (err == hipSuccess)
+            err = hipMemcpyAsync(d, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice, up);
+        if (err == hipSuccess) err = hipStreamSynchronize(up);  // landed before any launch reads it
+        if (up) (void)hipStreamDestroy(up);
+        if (err != hipSuccess) {
             if (d) (void)hipFree(d);
-            return set_error(STENCIL_EHIP, "packed schedule upload failed");
+            return set_error(STENCIL_EHIP, "packed schedule upload failed: %s", hipGetErrorString(err));
         }
-        e.table = d;
+        lock.lock();
+        if (e.table) (void)hipFree(d);  // another thread uploaded it meanwhile
+        else e.table = d;
     }
     *sched = e.table;
     *nb = e.workgroups;

@@ -8,6 +8,8 @@
 // include/stencil_hip.h documents in both.
 #include <cstdlib>
 
+#include "common.hpp"
+
 namespace stencil {
 
 static int env_or(const char* name, int dflt) {
@@ -25,6 +27,18 @@ int knob(const char* name, int dflt) {
 }
 
 int api_knob(const char* name, int dflt) { return env_or(name, dflt); }
+
+#ifndef STENCIL_DEBUG_KNOBS
+// The box code-generation probe (kernels_boxk_probe.hip, debug cfgs 95RRNN /
+// 96RRNN) is linked into the debug library only; the product library gets
+// these stubs, which its AUTO plan never reaches.
+int launch_boxk_probe_slp(const stencil_layout&, const void*, void*, int64_t, int64_t, int, int, hipStream_t) {
+    return set_error(STENCIL_EUNSUPPORTED, "the box probe shapes are in libstencil_hip_debug.so only");
+}
+int launch_boxk_probe_noslp(const stencil_layout&, const void*, void*, int64_t, int64_t, int, int, hipStream_t) {
+    return set_error(STENCIL_EUNSUPPORTED, "the box probe shapes are in libstencil_hip_debug.so only");
+}
+#endif
 
 }  // namespace stencil
 

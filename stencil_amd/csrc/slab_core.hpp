@@ -1,0 +1,771 @@
+// slab_core.hpp -- the multi-GPU z-slab job (include/stencil_hip.h part 3),
+// written once over a device backend.
+//
+// The reference runs its whole decomposed job behind one kernel call: 64
+// CPEs own 8x8 blocks, exchange halo strips by DMA / RMA every iteration and
+// meet at a barrier (athread_spawn/join, src/stencil/stencil.cpp:34-53; halo
+// DMA stencil_dma.cpp:236-247; barrier 562-563; RMA stencil_rma.cpp:198-255;
+// the block cut include/stencil/boundary_matrix.hpp:190-218).  Here the blocks
+// are contiguous z-slabs of the global grid, one per GPU (remainder planes to
+// the lowest slabs), each with K ghost planes per shared face, where K is the
+// number of sweeps stencil_iterate fuses into one launch for the problem
+// (7-point star: 4 or 5; box: 3 or 4): one round = K fused sweeps + one
+// exchange of K whole planes with each neighbour (temporal blocking across
+// GPUs; the halo planes are advanced on chip).  Every cell's arithmetic is
+// the single-grid kernel's: results are bitwise those of one grid.
+//
+// Three round forms:
+//   boundary + interior  stream A (high priority): the K boundary planes of
+//                        each face, then the exchange; stream B: the interior
+//                        meanwhile.
+//   face-signalled       ONE launch per slab whose workgroups storing the face
+//                        planes add to the slab's counters; the exchange
+//                        stream waits for the counts and sends while the rest
+//                        of the launch runs.
+//   rolling              ONE resident grid per slab plus a margin of spare
+//                        planes (stencil_rolling_*): a pass of
+//                        K sweeps is ceil(n / S) z-range launches writing the
+//                        new grid D planes down (or back up), then the
+//                        exchange -- for slabs whose two grids do not fit
+//                        (the north star's 4096^3 fp64 on 2 GPUs: one 278 GB
+//                        grid per GPU).
+// Exchange: RCCL ncclSend/ncclRecv inside one group spanning every slab this
+// process drives, or device copies (slabs may then share a GPU).
+//
+// `Dev` supplies streams, events, memory, the sweeps and the communicator:
+// csrc/slab.hip's HipDev (HIP + RCCL, the product) and the CPU test build's
+// fake device (tests/cpu_slab/: synchronous plane copies and the oracle's
+// sweep, an in-process mailbox for send/recv), which runs this same round
+// logic at world 2/3 under `pytest -m "not gpu"`.
+#pragma once
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "errors.hpp"
+#include "stencil_hip.h"
+
+namespace stencil {
+namespace slab {
+
+template <class Dev>
+struct Slab {
+    int device = 0;
+    int index = 0;             // global slab index (= communicator rank)
+    int64_t first = 0, n = 0;  // global first plane, planes owned
+    stencil_layout l{};
+    // two grids a / b; rolling: `a` is the one allocation (margin + grid), b null
+    void* a = nullptr;
+    void* b = nullptr;
+    typename Dev::Stream sa{}, sb{};  // boundary + exchange (high priority) / interior
+    typename Dev::Event ev_bnd{}, ev_int{}, ev_join{};
+    typename Dev::Comm comm{};
+    // face-signalled rounds: [0] low-face adds, [1] high-face adds (they run
+    // on across launches), [2] the wait kernel's timeout flag
+    uint32_t* counters = nullptr;
+    uint32_t sig_target = 0;  // adds per face expected once the last queued launch is done
+};
+
+template <class Dev>
+struct Job {
+    stencil_problem global{};
+    int exchange = STENCIL_EXCHANGE_RCCL;
+    bool periodic = false;
+    int k = 1;       // sweeps per round (fused launch depth)
+    int depth = 1;   // halo planes exchanged per face
+    bool cur_is_a = true;
+    bool chained = false;  // round events recorded since the last join
+    bool signal = false;   // full rounds as face-signalled single launches
+    int nranks = 0;        // rank mode: slabs of the job, this process owns s[0]
+    // rolling (STENCIL_SLAB_ROLLING): spare planes below each slab's grid;
+    // position 0 = the grid at home (allocation offset `margin` planes), 1 =
+    // shifted to the allocation's start
+    int64_t margin = 0;
+    int position = 0;
+    std::vector<Slab<Dev>> s;
+    // kernel timing: events around slab 0's compute launch(es) of every round
+    bool timing = false;
+    std::vector<std::pair<typename Dev::Event, typename Dev::Event>> tev;
+    int64_t timed_cells = 0;
+    int64_t timed_launches = 0;  // kernel launches inside the timed spans
+};
+
+#define SLAB_TRY(expr)               \
+    do {                             \
+        if (int rc_ = (expr)) return rc_; \
+    } while (0)
+
+// ---- geometry -------------------------------------------------------------
+template <class Dev>
+inline size_t elem_bytes(const Slab<Dev>& s) { return s.l.prob.dtype == STENCIL_F64 ? 8 : 4; }
+template <class Dev>
+inline size_t plane_bytes(const Slab<Dev>& s) { return size_t(s.l.plane) * elem_bytes(s); }
+// first byte of plane z of the grid based at `grid` (z may be a ghost/halo plane)
+template <class Dev>
+inline char* plane_ptr(const Slab<Dev>& s, void* grid, int64_t z) {
+    return static_cast<char*>(grid) + size_t(s.l.zghost + z) * plane_bytes(s);
+}
+// the grid of slab s at rolling position `pos` (two grids: a for pos 0, b for 1)
+template <class Dev>
+inline void* grid_at(const Job<Dev>& j, const Slab<Dev>& s, int pos) {
+    if (j.margin == 0) return pos == 0 ? s.a : s.b;
+    return pos == 0 ? static_cast<char*>(s.a) + size_t(j.margin) * plane_bytes(s) : s.a;
+}
+template <class Dev>
+inline int cur_pos(const Job<Dev>& j) { return j.margin ? j.position : (j.cur_is_a ? 0 : 1); }
+template <class Dev>
+inline void* cur_grid(const Job<Dev>& j, const Slab<Dev>& s) { return grid_at(j, s, cur_pos(j)); }
+
+// neighbours of global slab i (its communicator peers); -1: a global end
+template <class Dev>
+inline int slabs_total(const Job<Dev>& j) { return j.nranks ? j.nranks : int(j.s.size()); }
+template <class Dev>
+inline int lo_nb(const Job<Dev>& j, int i) {
+    return i > 0 ? i - 1 : (j.periodic ? slabs_total(j) - 1 : -1);
+}
+template <class Dev>
+inline int hi_nb(const Job<Dev>& j, int i) {
+    const int n = slabs_total(j);
+    return i < n - 1 ? i + 1 : (j.periodic ? 0 : -1);
+}
+
+// ---- timing ---------------------------------------------------------------
+template <class Dev>
+int time_begin(Job<Dev>& j, size_t slab, typename Dev::Stream st) {
+    if (!j.timing || slab != 0) return STENCIL_OK;
+    typename Dev::Event a{}, b{};
+    SLAB_TRY(Dev::event_create(&a, true));
+    if (int rc = Dev::event_create(&b, true)) {
+        Dev::event_destroy(a);
+        return rc;
+    }
+    j.tev.emplace_back(a, b);
+    return Dev::event_record(a, st);
+}
+template <class Dev>
+int time_end(Job<Dev>& j, size_t slab, typename Dev::Stream st, int64_t cells, int64_t launches) {
+    if (!j.timing || slab != 0) return STENCIL_OK;
+    j.timed_cells = cells;
+    j.timed_launches += launches;
+    return Dev::event_record(j.tev.back().second, st);
+}
+template <class Dev>
+void drop_timing(Job<Dev>& j) {
+    for (auto& e : j.tev) {
+        Dev::event_destroy(e.first);
+        Dev::event_destroy(e.second);
+    }
+    j.tev.clear();
+    j.timed_cells = 0;
+    j.timed_launches = 0;
+}
+
+// ---- exchange -------------------------------------------------------------
+// Halo exchange of the grids at rolling position `pos` (each slab's copy of
+// the same logical grid): every slab's `depth` face planes into its
+// neighbours' halo planes, queued on the slabs' A streams behind what is
+// already there.  Faces are contiguous whole planes: nothing is packed.
+template <class Dev>
+int exchange(Job<Dev>& j, int pos) {
+    const int n = int(j.s.size());
+    const int64_t d = j.depth;
+    if (j.exchange == STENCIL_EXCHANGE_RCCL) {
+        SLAB_TRY(Dev::group_start());
+        int rc = STENCIL_OK;
+        for (int i = 0; i < n && rc == STENCIL_OK; ++i) {
+            Slab<Dev>& s = j.s[size_t(i)];
+            void* g = grid_at(j, s, pos);
+            const size_t bytes = size_t(d) * plane_bytes(s);
+            const int lo = lo_nb(j, s.index), hi = hi_nb(j, s.index);
+            // sends and receives to one peer match in posting order: a slab
+            // that is its own neighbour (periodic, N = 1) sends hi -> recv lo
+            // first, then lo -> hi
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, s.n - d), bytes, hi, s.comm, s.sa);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, -d), bytes, lo, s.comm, s.sa);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, 0), bytes, lo, s.comm, s.sa);
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, s.n), bytes, hi, s.comm, s.sa);
+        }
+        const int rc2 = Dev::group_end();
+        return rc != STENCIL_OK ? rc : rc2;
+    }
+    // device copies (single-process jobs only: local = global index): slab i's
+    // A stream pulls its neighbours' faces once their round is complete
+    // (ev_join, recorded on their A streams after joining B)
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ev_join, s.sa));
+    }
+    for (int i = 0; i < n; ++i) {
+        Slab<Dev>& s = j.s[size_t(i)];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* g = grid_at(j, s, pos);
+        const size_t bytes = size_t(d) * plane_bytes(s);
+        const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+        if (lo >= 0) {
+            Slab<Dev>& t = j.s[size_t(lo)];
+            SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
+            SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, -d), s.device, plane_ptr(t, grid_at(j, t, pos), t.n - d), t.device,
+                                    bytes, s.sa));
+        }
+        if (hi >= 0) {
+            Slab<Dev>& t = j.s[size_t(hi)];
+            SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
+            SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, s.n), s.device, plane_ptr(t, grid_at(j, t, pos), 0), t.device, bytes,
+                                    s.sa));
+        }
+    }
+    return STENCIL_OK;
+}
+
+template <class Dev>
+int sync_all(Job<Dev>& j) {
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::stream_sync(s.sa));
+        SLAB_TRY(Dev::stream_sync(s.sb));
+    }
+    j.chained = false;
+    return STENCIL_OK;
+}
+
+// ---- rounds ---------------------------------------------------------------
+// One round of `k` fused sweeps: src -> dst on every slab, then the exchange
+// of dst's faces.  Boundary planes on A (the exchange queued behind them),
+// the interior on B.
+template <class Dev>
+int slab_round(Job<Dev>& j, int k) {
+    const int src_pos = cur_pos(j), dst_pos = 1 - src_pos;
+    const int64_t edge = j.depth;
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        void* dst = grid_at(j, s, dst_pos);
+        if (j.chained) {
+            // interior(r) reads src [0, n): after boundary + exchange(r-1);
+            // boundary(r) overwrites planes interior(r-1) read: after it
+            SLAB_TRY(Dev::stream_wait(s.sb, s.ev_bnd));
+            SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
+        }
+        const int64_t plane_cells = s.l.prob.nx * s.l.prob.ny;
+        if (s.n > 2 * edge) {
+            SLAB_TRY(time_begin(j, i, s.sb));
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, edge, s.n - edge, k, s.sb));
+            SLAB_TRY(time_end(j, i, s.sb, plane_cells * (s.n - 2 * edge), 1));
+            SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, 0, edge, k, s.sa));
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, s.n - edge, s.n, k, s.sa));
+        } else {
+            SLAB_TRY(time_begin(j, i, s.sa));
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, 0, s.n, k, s.sa));
+            SLAB_TRY(time_end(j, i, s.sa, plane_cells * s.n, 1));
+            SLAB_TRY(Dev::event_record(s.ev_int, s.sa));
+        }
+        if (j.exchange == STENCIL_EXCHANGE_COPY)  // the face copies read whole rounds
+            SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
+    }
+    SLAB_TRY(exchange(j, dst_pos));
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ev_bnd, s.sa));
+    }
+    j.chained = true;
+    j.cur_is_a = dst_pos == 0;
+    return STENCIL_OK;
+}
+
+// One round of `k` fused sweeps as ONE face-signalled launch per slab
+// (stencil_sweepk_signal): the launch's first z-chunk marches
+// up and its last down, so its face planes are among the first stored; the
+// workgroups storing them add to the slab's counters.  The exchange stream
+// queues a wait for the counts and the halo exchange behind it, so the faces
+// leave while the rest of the launch runs.  Order: launch(r) reads the halos
+// exchange(r-1) received (B waits for A); exchange(r) receives into the halo
+// planes launch(r-1) read, and starts only once launch(r) has signalled,
+// i.e. after launch(r-1) ended (one stream).
+template <class Dev>
+int slab_round_signal(Job<Dev>& j, int k) {
+    const int src_pos = cur_pos(j), dst_pos = 1 - src_pos;
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        void* dst = grid_at(j, s, dst_pos);
+        if (j.chained) SLAB_TRY(Dev::stream_wait(s.sb, s.ev_bnd));
+        int nsig = 0;
+        SLAB_TRY(time_begin(j, i, s.sb));
+        SLAB_TRY(Dev::sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, &nsig, s.sb));
+        SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, 1));
+        SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
+        s.sig_target += uint32_t(nsig);
+        SLAB_TRY(Dev::wait_counters(s.counters, s.sig_target, s.sig_target, s.sa));
+    }
+    SLAB_TRY(exchange(j, dst_pos));
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ev_bnd, s.sa));
+        // the next round's boundary-launch path (remainders) writes planes
+        // this launch reads: A must also follow B
+        SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
+    }
+    j.chained = true;
+    j.cur_is_a = dst_pos == 0;
+    return STENCIL_OK;
+}
+
+// Launches per pass of a rolling slab: z-ranges of S = margin - K*r planes.
+template <class Dev>
+inline int64_t rolling_span(const Job<Dev>& j) { return j.margin - int64_t(j.k) * j.global.radius; }
+
+// One rolling pass of `k` sweeps on every slab (the single-GPU scheme of
+// stencil_rolling_iterate, api.hip, per slab): from home the new grid goes D
+// planes down, launches bottom-up; from the shifted position back up,
+// launches top-down.  A launch over [jS, jS + S) reads slots [jS - kr,
+// jS + S + kr) and writes [jS - D, jS + S - D) (down): disjoint, and no later
+// launch of the pass reads what it writes.  Then the new grid's halo planes:
+// a shared face's from the neighbour (the exchange, queued behind the pass on
+// the same stream, so it starts once every launch that reads those slots is
+// done), a global end's ghost planes by one plane copy from the slots no pass
+// writes (the shifted grid's bottom ghosts, the home grid's top ghosts).
+template <class Dev>
+int slab_round_rolling(Job<Dev>& j, int k) {
+    const int64_t S = rolling_span(j);
+    const bool down = j.position == 0;
+    const int src_pos = j.position, dst_pos = 1 - j.position;
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        void* dst = grid_at(j, s, dst_pos);
+        const int64_t J = (s.n + S - 1) / S;
+        SLAB_TRY(time_begin(j, i, s.sa));
+        for (int64_t q = 0; q < J; ++q) {
+            const int64_t jj = down ? q : J - 1 - q;
+            const int64_t b = jj * S, e = std::min(s.n, b + S);
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, b, e, k, s.sa));
+        }
+        SLAB_TRY(time_end(j, i, s.sa, s.l.prob.nx * s.l.prob.ny * s.n, J));
+        const int64_t zg = s.l.zghost;
+        const size_t pb = plane_bytes(s);
+        const bool has_lo = lo_nb(j, s.index) >= 0, has_hi = hi_nb(j, s.index) >= 0;
+        if (down && !has_hi)  // the shifted grid's top ghosts from the home grid's (never written)
+            SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, s.n), plane_ptr(s, src, s.n), size_t(zg) * pb, s.sa));
+        if (!down && !has_lo)  // the home grid's bottom ghosts from the shifted grid's (never written)
+            SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, -zg), plane_ptr(s, src, -zg), size_t(zg) * pb, s.sa));
+    }
+    SLAB_TRY(exchange(j, dst_pos));
+    j.position = dst_pos;
+    j.chained = false;  // one stream per slab: nothing to chain
+    return STENCIL_OK;
+}
+
+// Did a face-counter wait give up?  Then the halos are wrong.
+template <class Dev>
+int check_signal_timeouts(Job<Dev>& j) {
+    for (Slab<Dev>& s : j.s) {
+        if (!s.counters) continue;
+        SLAB_TRY(Dev::set_device(s.device));
+        bool timed_out = false;
+        SLAB_TRY(Dev::read_timeout(s.counters, &timed_out));
+        if (timed_out) return set_error(STENCIL_EHIP, "slab on device %d: a face-counter wait timed out", s.device);
+    }
+    return STENCIL_OK;
+}
+
+// ---- lifetime -------------------------------------------------------------
+template <class Dev, class JobT>
+void release(JobT* j) {
+    if (!j) return;
+    if (!j->s.empty()) {
+        (void)Dev::set_device(j->s[0].device);
+        drop_timing(*j);
+    }
+    for (Slab<Dev>& s : j->s) {
+        (void)Dev::set_device(s.device);
+        if (s.sa) (void)Dev::stream_sync(s.sa);
+        if (s.sb) (void)Dev::stream_sync(s.sb);
+        if (s.comm) Dev::comm_destroy(s.comm);
+        if (s.a) Dev::free(s.a);
+        if (s.b) Dev::free(s.b);
+        if (s.sa) Dev::stream_destroy(s.sa);
+        if (s.sb) Dev::stream_destroy(s.sb);
+        if (s.ev_bnd) Dev::event_destroy(s.ev_bnd);
+        if (s.ev_int) Dev::event_destroy(s.ev_int);
+        if (s.ev_join) Dev::event_destroy(s.ev_join);
+        if (s.counters) Dev::free_counters(s.counters);
+    }
+    delete j;
+}
+
+// Sweeps stencil_iterate fuses into one launch for `p`: the round length.
+// Margin (spare planes) of a rolling slab whose layout is `l`: `want` > 0 as
+// asked; 0 = as deep as the device's free memory allows beside the grid, less
+// a reserve for the communicator, at most 512 planes.
+template <class Dev>
+int rolling_margin(const Job<Dev>& j, const stencil_layout& l, int64_t want, int64_t* out) {
+    const int64_t reach = int64_t(j.k) * j.global.radius;
+    const int64_t pb = l.plane * (l.prob.dtype == STENCIL_F64 ? 8 : 4);
+    int64_t m = want;
+    if (m <= 0) {
+        int64_t free_b = 0;
+        SLAB_TRY(Dev::free_bytes(&free_b));
+        const int64_t reserve = int64_t(4) << 30;
+        m = std::min<int64_t>(512, (free_b - l.bytes - reserve - 256) / pb);
+        if (m < 4 * (reach + 1))
+            return set_error(STENCIL_ENOMEM, "rolling slab: %lld GB grid + a margin of %lld planes do not fit %lld GB free",
+                             (long long)(l.bytes / 1000000000), (long long)(4 * (reach + 1)),
+                             (long long)(free_b / 1000000000));
+    }
+    if (m < reach + 1)
+        return set_error(STENCIL_EINVAL, "rolling slab margin must be at least %lld planes (got %lld)",
+                         (long long)(reach + 1), (long long)m);
+    *out = m;
+    return STENCIL_OK;
+}
+
+// The slabs this process owns: global slab indices `idx` (of `total`) on
+// `devs`; the z split is the same in every process (planes total / N, the first
+// nz % N slabs one more), so each rank can build its own share alone.
+template <class Dev, class JobT>
+int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, const std::vector<int>& devs,
+              int32_t exchange_kind, int32_t flags, int64_t margin, bool rank_mode, JobT** out) {
+    auto* j = new JobT;
+    j->global = g;
+    j->exchange = exchange_kind;
+    j->periodic = flags & STENCIL_SLAB_PERIODIC;
+    j->nranks = rank_mode ? total : 0;
+    j->k = Dev::fuse_depth(g);
+    j->depth = std::max<int>(j->k, g.radius);
+    const bool rolling = flags & STENCIL_SLAB_ROLLING;
+    // face-signalled rounds where the K-step kernels have them (3D r = 1 naive
+    // 7-point star K = 3..5, box K = 2..4), two-grid slabs only; the product's
+    // STENCIL_SLAB_SIGNAL=0: boundary + interior launches
+    {
+        const bool star = g.shape == STENCIL_STAR && j->k >= 3 && j->k <= 5;
+        const bool box = g.shape == STENCIL_BOX && j->k >= 2 && j->k <= 4;
+        // and only with one slab per GPU: slabs sharing a GPU multiplex their
+        // streams onto its few hardware queues, where a polling wait kernel
+        // could sit in front of the launch another slab's wait is polling for
+        // (ranks each own one GPU: RCCL refuses two ranks on one device)
+        bool distinct = true;
+        for (size_t i = 0; i < devs.size(); ++i)
+            for (size_t q = 0; q < i; ++q) distinct = distinct && devs[i] != devs[q];
+        j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct && !rolling &&
+                    Dev::signal_enabled();
+    }
+    const int64_t base = g.nz / total, rem = g.nz % total;
+    // the smallest slab of the job decides, the same in every process: ranks
+    // of one job all reject it here, before any of them enters the
+    // communicator's collective init (a rank that failed alone would leave
+    // the others waiting in the bootstrap)
+    if (base < j->depth) {
+        const int rc = set_error(STENCIL_EINVAL, "%d slabs of %lld planes: the smallest owns %lld planes < the %d halo "
+                                 "planes: use fewer GPUs", total, (long long)g.nz, (long long)base, j->depth);
+        delete j;
+        return rc;
+    }
+    j->s.resize(idx.size());
+    int rc = STENCIL_OK;
+    for (size_t li = 0; li < idx.size() && rc == STENCIL_OK; ++li) {
+        const int i = idx[li];
+        Slab<Dev>& s = j->s[li];
+        s.index = i;
+        s.device = devs[li];
+        s.n = base + (i < rem ? 1 : 0);
+        s.first = i * base + std::min<int64_t>(i, rem);
+        stencil_problem p = g;
+        p.nz = s.n;
+        p.halo = j->depth;
+        p.flags = (lo_nb(*j, i) >= 0 ? STENCIL_HALO_LO : 0) | (hi_nb(*j, i) >= 0 ? STENCIL_HALO_HI : 0);
+        if ((rc = Dev::layout_init(&p, &s.l))) break;
+        if ((rc = Dev::set_device(s.device))) break;
+        if (rolling) {
+            int64_t m = 0;
+            if ((rc = rolling_margin(*j, s.l, margin, &m))) break;
+            // one margin for the job (the largest slab decides when sized from free memory)
+            if (li == 0 || m < j->margin) j->margin = m;
+            const int64_t bytes = (s.l.planes + m) * int64_t(plane_bytes(s)) + 256;
+            if ((rc = Dev::alloc(bytes, &s.a))) break;
+        } else {
+            if ((rc = Dev::alloc(s.l.bytes + 256, &s.a)) || (rc = Dev::alloc(s.l.bytes + 256, &s.b))) break;
+        }
+        if ((rc = Dev::stream_create(&s.sa, true)) || (rc = Dev::stream_create(&s.sb, false)) ||
+            (rc = Dev::event_create(&s.ev_bnd, false)) || (rc = Dev::event_create(&s.ev_int, false)) ||
+            (rc = Dev::event_create(&s.ev_join, false)))
+            break;
+        if ((rc = Dev::alloc_counters(&s.counters))) break;
+    }
+    if (rc != STENCIL_OK) {
+        release<Dev>(j);
+        return rc;
+    }
+    *out = j;
+    return STENCIL_OK;
+}
+
+template <class Dev>
+int check_global(const stencil_problem* global, stencil_problem* g, int32_t flags) {
+    *g = *global;
+    if (g->dims != 3) return set_error(STENCIL_EUNSUPPORTED, "slab jobs split 3D grids along z");
+    if (g->halo != 0 || g->flags != 0) return set_error(STENCIL_EINVAL, "the global problem takes no halo / flags");
+    if (flags & ~(STENCIL_SLAB_PERIODIC | STENCIL_SLAB_ROLLING)) return set_error(STENCIL_EINVAL, "bad slab flags %d", flags);
+    stencil_layout gl;
+    return Dev::layout_init(g, &gl);
+}
+
+// ---- the C-ABI's bodies -----------------------------------------------------
+template <class Dev, class JobT>
+int create(const stencil_problem* global, int32_t ngpus, const int32_t* devices, int32_t exchange_kind, int32_t flags,
+           int64_t margin, JobT** job) {
+    if (!global || !job || ngpus < 1) return set_error(STENCIL_EINVAL, "null argument or ngpus < 1");
+    *job = nullptr;
+    if (exchange_kind != STENCIL_EXCHANGE_RCCL && exchange_kind != STENCIL_EXCHANGE_COPY)
+        return set_error(STENCIL_EINVAL, "bad exchange kind %d", exchange_kind);
+    stencil_problem g;
+    SLAB_TRY(check_global<Dev>(global, &g, flags));
+    std::vector<int> devs(static_cast<size_t>(ngpus)), idx(static_cast<size_t>(ngpus));
+    for (int i = 0; i < ngpus; ++i) {
+        devs[size_t(i)] = devices ? devices[i] : i;
+        idx[size_t(i)] = i;
+    }
+    if (exchange_kind == STENCIL_EXCHANGE_RCCL) {
+        for (int i = 0; i < ngpus; ++i)
+            for (int q = 0; q < i; ++q)
+                if (devs[size_t(i)] == devs[size_t(q)])
+                    return set_error(STENCIL_EINVAL, "RCCL needs one slab per GPU (device %d twice): use device copies",
+                                     devs[size_t(i)]);
+        if (!Dev::comm_available()) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
+    }
+    JobT* j = nullptr;
+    SLAB_TRY((build_job<Dev, JobT>(g, ngpus, idx, devs, exchange_kind, flags, margin, false, &j)));
+    if (exchange_kind == STENCIL_EXCHANGE_RCCL) {
+        std::vector<typename Dev::Comm> comms(static_cast<size_t>(ngpus), typename Dev::Comm{});
+        if (int rc = Dev::comm_init_all(comms.data(), ngpus, devs.data())) {
+            release<Dev>(j);
+            return rc;
+        }
+        for (int i = 0; i < ngpus; ++i) j->s[size_t(i)].comm = comms[size_t(i)];
+    }
+    *job = j;
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int32_t device, const void* id,
+                int64_t id_bytes, int32_t flags, int64_t margin, JobT** job) {
+    if (!global || !job || !id) return set_error(STENCIL_EINVAL, "null argument");
+    *job = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(STENCIL_EINVAL, "rank %d of %d", rank, nranks);
+    if (id_bytes != STENCIL_SLAB_ID_BYTES)
+        return set_error(STENCIL_EINVAL, "the id holds %d bytes, not %lld", int(STENCIL_SLAB_ID_BYTES),
+                         (long long)id_bytes);
+    stencil_problem g;
+    SLAB_TRY(check_global<Dev>(global, &g, flags));
+    if (!Dev::comm_available()) return set_error(STENCIL_EUNSUPPORTED, "librccl could not be loaded");
+    JobT* j = nullptr;
+    SLAB_TRY((build_job<Dev, JobT>(g, nranks, {rank}, {device}, STENCIL_EXCHANGE_RCCL, flags, margin, true, &j)));
+    if (int rc = Dev::set_device(device)) {
+        release<Dev>(j);
+        return rc;
+    }
+    // collective over the ranks: every rank must reach it (build_job's
+    // checks that depend on the global problem fail on every rank alike)
+    typename Dev::Comm comm{};
+    if (int rc = Dev::comm_init_rank(&comm, nranks, id, rank)) {
+        release<Dev>(j);
+        return rc;
+    }
+    j->s[0].comm = comm;
+    *job = j;
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int info(const JobT* job, int32_t slab, int64_t* first_plane, int64_t* planes, int32_t* device, int32_t* sweeps) {
+    if (!job || slab < 0 || slab >= int(job->s.size())) return set_error(STENCIL_EINVAL, "bad job or slab index");
+    const Slab<Dev>& s = job->s[size_t(slab)];
+    if (first_plane) *first_plane = s.first;
+    if (planes) *planes = s.n;
+    if (device) *device = s.device;
+    if (sweeps) *sweeps = job->k;
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int rolling_info(const JobT* job, int64_t* margin, int64_t* launches_per_pass) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    if (margin) *margin = job->margin;
+    if (launches_per_pass) {
+        int64_t most = 0;
+        if (job->margin)
+            for (const Slab<Dev>& s : job->s) most = std::max(most, (s.n + rolling_span(*job) - 1) / rolling_span(*job));
+        *launches_per_pass = most;
+    }
+    return STENCIL_OK;
+}
+
+// The margin's spare slots of a rolling slab get a copy of the home grid's
+// plane -1 (as stencil_rolling_init_margin copies a ghost plane): every plane
+// then has the same x/y ghost ring, the reference initial condition's
+// invariant, and the shifted grid's bottom planes [-zg, 0) -- slots no pass
+// writes -- hold the global bottom ghost plane on the first slab (a halo
+// elsewhere, received before it is read).  Called before the halo exchange.
+template <class Dev>
+int init_margin(const Job<Dev>& j, Slab<Dev>& s) {
+    if (!j.margin) return STENCIL_OK;
+    void* home = grid_at(j, s, 0);
+    const size_t pb = plane_bytes(s);
+    for (int64_t i = 0; i < j.margin; ++i)
+        SLAB_TRY(Dev::copy_d2d(static_cast<char*>(s.a) + size_t(i) * pb, plane_ptr(s, home, -1), pb, s.sa));
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int fill_initial(JobT* job, int32_t init_kind, uint64_t seed) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    SLAB_TRY(sync_all(*job));
+    job->cur_is_a = true;
+    job->position = 0;
+    for (Slab<Dev>& s : job->s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        // global linear indices: the slab's interior starts first * nx * ny cells in
+        const uint64_t sd = seed + uint64_t(s.first) * uint64_t(s.l.prob.nx) * uint64_t(s.l.prob.ny);
+        SLAB_TRY(Dev::fill_initial(&s.l, grid_at(*job, s, 0), init_kind, sd, s.sa));
+        if (job->margin)
+            SLAB_TRY(init_margin(*job, s));
+        else
+            SLAB_TRY(Dev::fill_initial(&s.l, s.b, init_kind, sd, s.sa));
+    }
+    // the halos: the neighbours' faces (ghost planes otherwise)
+    SLAB_TRY(exchange(*job, 0));
+    if (!job->margin) SLAB_TRY(exchange(*job, 1));
+    return sync_all(*job);
+}
+
+template <class Dev, class JobT>
+int upload(JobT* job, const void* host, int64_t host_row, int64_t host_rows) {
+    if (!job || !host) return set_error(STENCIL_EINVAL, "null argument");
+    const stencil_problem& g = job->global;
+    if (host_row < g.nx + 2 * g.radius || host_rows < g.ny + 2 * g.radius)
+        return set_error(STENCIL_EINVAL, "host array too small");
+    SLAB_TRY(sync_all(*job));
+    const size_t es = g.dtype == STENCIL_F64 ? 8 : 4;
+    job->cur_is_a = true;
+    job->position = 0;
+    for (Slab<Dev>& s : job->s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        // host planes [first, first + n + 2r) hold this slab's planes -r .. n+r-1
+        const char* h = static_cast<const char*>(host) + size_t(s.first) * size_t(host_row * host_rows) * es;
+        SLAB_TRY(Dev::upload(&s.l, grid_at(*job, s, 0), h, host_row, host_rows, s.sa));
+        if (job->margin)
+            SLAB_TRY(init_margin(*job, s));
+        else
+            SLAB_TRY(Dev::upload(&s.l, s.b, h, host_row, host_rows, s.sa));
+    }
+    SLAB_TRY(exchange(*job, 0));
+    if (!job->margin) SLAB_TRY(exchange(*job, 1));
+    return sync_all(*job);
+}
+
+template <class Dev, class JobT>
+int run(JobT* job, uint32_t iterations, float* elapsed_ms) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    SLAB_TRY(sync_all(*job));
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t done = 0;
+    const uint32_t k = uint32_t(job->k);
+    for (; done + k <= iterations; done += k)
+        SLAB_TRY(job->margin ? slab_round_rolling(*job, int(k))
+                             : job->signal ? slab_round_signal(*job, int(k)) : slab_round(*job, int(k)));
+    if (done < iterations)  // the remainder as one shorter fused round
+        SLAB_TRY(job->margin ? slab_round_rolling(*job, int(iterations - done))
+                             : slab_round(*job, int(iterations - done)));
+    SLAB_TRY(sync_all(*job));
+    if (job->signal) SLAB_TRY(check_signal_timeouts(*job));
+    const auto t1 = std::chrono::steady_clock::now();
+    if (elapsed_ms) *elapsed_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int download(JobT* job, void* host, int64_t host_row, int64_t host_rows) {
+    if (!job || !host) return set_error(STENCIL_EINVAL, "null argument");
+    SLAB_TRY(sync_all(*job));
+    const stencil_problem& g = job->global;
+    const int64_t r = g.radius;
+    const size_t es = g.dtype == STENCIL_F64 ? 8 : 4;
+    const size_t hplane = size_t(host_row * host_rows) * es;
+    if (host_row < g.nx + 2 * r || host_rows < g.ny + 2 * r) return set_error(STENCIL_EINVAL, "host array too small");
+    std::vector<char> tmp;
+    for (Slab<Dev>& s : job->s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        // the slab's planes -r .. n+r-1 through a scratch copy; keep its own
+        // planes, plus the global ghost planes at the two ends
+        tmp.resize(size_t(s.n + 2 * r) * hplane);
+        SLAB_TRY(Dev::download(&s.l, cur_grid(*job, s), tmp.data(), host_row, host_rows, s.sa));
+        SLAB_TRY(Dev::stream_sync(s.sa));
+        const int64_t z0 = s.index == 0 ? -r : 0;
+        const int64_t z1 = s.index + 1 == slabs_total(*job) ? s.n + r : s.n;
+        std::memcpy(static_cast<char*>(host) + size_t(s.first + z0 + r) * hplane, tmp.data() + size_t(z0 + r) * hplane,
+                    size_t(z1 - z0) * hplane);
+    }
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int kernel_timing(JobT* job, int32_t enable) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(Dev::set_device(job->s[0].device));
+    drop_timing(*job);
+    job->timing = enable != 0;
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int kernel_time(JobT* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch, int32_t* signalled) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(Dev::set_device(job->s[0].device));
+    float sum = 0.f;
+    for (auto& e : job->tev) {
+        float ms = 0.f;
+        SLAB_TRY(Dev::event_elapsed(&ms, e.first, e.second));
+        sum += ms;
+    }
+    if (total_ms) *total_ms = sum;
+    // a timed span is one launch, or (rolling) the pass's launches: reported
+    // per span, so `cells_per_launch` is what one span covers
+    if (launches) *launches = int64_t(job->tev.size());
+    if (cells_per_launch) *cells_per_launch = job->timed_cells;
+    if (signalled) *signalled = job->signal ? 1 : job->margin ? 2 : 0;
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int plane_sums(JobT* job, double* sums) {
+    if (!job || !sums) return set_error(STENCIL_EINVAL, "null argument");
+    SLAB_TRY(sync_all(*job));
+    for (Slab<Dev>& s : job->s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::plane_sums(&s.l, cur_grid(*job, s), sums + s.first, s.sa));
+        SLAB_TRY(Dev::stream_sync(s.sa));
+    }
+    clear_error();
+    return STENCIL_OK;
+}
+
+#undef SLAB_TRY
+
+}  // namespace slab
+}  // namespace stencil

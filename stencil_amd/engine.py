@@ -347,38 +347,41 @@ class SlabJob:
     per-process driver for callers without torch.distributed."""
 
     def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int, devices, exchange: str = "rccl",
-                 periodic: bool = False, rank=None):
+                 periodic: bool = False, rank=None, rolling: bool = False, margin: int = 0, lib=None):
         """rank=(nranks, rank, unique_id): rank mode (stencil_slab_create_rank),
         this process's one slab on devices[0], the others in other processes
         that make the same call with the same id (SlabJob.unique_id on one rank,
-        handed to the rest by the caller)."""
-        self.lib = _lib.load()
+        handed to the rest by the caller).  rolling: ONE grid per slab plus
+        `margin` spare planes (0: as deep as free memory allows).  lib: the
+        library whose stencil_slab_* entry points run the job (default the
+        product; the CPU tests pass tests/cpu_slab's fake device)."""
+        self.lib = lib if lib is not None else _lib.load()
         self.spec = spec
         self.shape = (nx, ny, nz)
         prob = spec.problem(nx, ny, nz)
         job = ctypes.c_void_p()
-        flags = _lib.SLAB_PERIODIC if periodic else 0
+        flags = (_lib.SLAB_PERIODIC if periodic else 0) | (_lib.SLAB_ROLLING if rolling else 0)
         if rank is not None:
             nranks, r, uid = rank
             if exchange != "rccl" or len(devices) != 1:
                 raise ValueError("rank mode: one device per rank, RCCL exchange")
             buf = ctypes.create_string_buffer(bytes(uid), len(uid))
-            _lib.check(self.lib.stencil_slab_create_rank(ctypes.byref(prob), nranks, r, devices[0], buf, len(uid),
-                                                         flags, ctypes.byref(job)),
+            _lib.check(self.lib.stencil_slab_create_rank2(ctypes.byref(prob), nranks, r, devices[0], buf, len(uid),
+                                                          flags, margin, ctypes.byref(job)),
                        "stencil_slab_create_rank", lib=self.lib)
         else:
             devs = (ctypes.c_int32 * len(devices))(*devices)
             kind = _lib.EXCHANGE_RCCL if exchange == "rccl" else _lib.EXCHANGE_COPY
-            _lib.check(self.lib.stencil_slab_create(ctypes.byref(prob), len(devices), devs, kind, flags,
-                                                    ctypes.byref(job)),
+            _lib.check(self.lib.stencil_slab_create2(ctypes.byref(prob), len(devices), devs, kind, flags, margin,
+                                                     ctypes.byref(job)),
                        "stencil_slab_create", lib=self.lib)
         self.job = job
         self.nslabs = len(devices)
 
     @staticmethod
-    def unique_id() -> bytes:
+    def unique_id(lib=None) -> bytes:
         """A fresh RCCL id for a rank-mode job (make it on one rank only)."""
-        lib = _lib.load()
+        lib = lib if lib is not None else _lib.load()
         buf = ctypes.create_string_buffer(_lib.SLAB_ID_BYTES)
         _lib.check(lib.stencil_slab_unique_id(buf, _lib.SLAB_ID_BYTES), "stencil_slab_unique_id", lib=lib)
         return buf.raw
@@ -401,6 +404,14 @@ class SlabJob:
                                               ctypes.byref(dev), ctypes.byref(k)), "stencil_slab_info", lib=self.lib)
         return {"first": int(first.value), "planes": int(planes.value), "device": int(dev.value),
                 "sweeps_per_round": int(k.value)}
+
+    def rolling_info(self) -> dict:
+        """Rolling slabs: the margin (0: two grids) and the most z-range
+        launches one pass makes on a slab of this process."""
+        m, n = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.check(self.lib.stencil_slab_rolling_info(self.job, ctypes.byref(m), ctypes.byref(n)),
+                   "stencil_slab_rolling_info", lib=self.lib)
+        return {"margin": int(m.value), "launches_per_pass": int(n.value)}
 
     def fill_initial(self, kind: str = "reference", seed: int = 0) -> None:
         k = _lib.INIT_RANDOM if kind == "random" else _lib.INIT_REFERENCE
@@ -439,8 +450,9 @@ class SlabJob:
         ms, n, cells, sig = ctypes.c_float(0.0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
         _lib.check(self.lib.stencil_slab_kernel_time(self.job, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(cells),
                                                      ctypes.byref(sig)), "stencil_slab_kernel_time", lib=self.lib)
+        # the round form: 0 boundary + interior launches, 1 face-signalled, 2 rolling passes
         return {"total_ms": float(ms.value), "launches": int(n.value), "cells_per_launch": int(cells.value),
-                "signalled": bool(sig.value)}
+                "signalled": int(sig.value) == 1, "rolling": int(sig.value) == 2}
 
     def plane_sums(self) -> np.ndarray:
         out = np.zeros(self.shape[2], dtype=np.float64)

@@ -1,0 +1,475 @@
+// fake_dev.cpp -- TEST INFRASTRUCTURE ONLY: a CPU "device" for slab_core.hpp,
+// so that the multi-GPU slab job's round and exchange logic -- the very code
+// csrc/slab.hip runs on the 8-GPU node -- runs under `pytest -m "not gpu"`.
+//
+//   memory     host allocations in the library's padded layout (the same
+//              stencil_layout arithmetic as api.hip's stencil_layout_init)
+//   streams    synchronous: every operation completes when it is issued, so
+//              events are host timestamps and waits are no-ops; what is
+//              checked is the data flow -- which planes each round sweeps,
+//              sends, receives and restores -- not stream concurrency
+//   sweeps     stencil_sweepk's contract (K fused sweeps of [begin, end), halo
+//              planes advanced, ghost cells never written) computed with the
+//              ORACLE (oracle/oracle.c): the planes [begin - K r, end + K r)
+//              are cut out as a dense ghost-padded sub-grid and swept K times;
+//              the cut ends stand still like ghost planes, which reaches K r
+//              planes inward after K sweeps and so never [begin, end)
+//   face-signalled launches: the sweep plus one add per face to the counters
+//   communicator: an in-process mailbox, one FIFO per (communicator id,
+//              sender, receiver) -- sends are buffered copies, receives match
+//              in posting order as NCCL's do, a group's receives complete at
+//              its end (blocking, with a timeout instead of a hang); rank-mode
+//              jobs in several threads of one process join by their id
+//
+// Exported with the fake_slab_ prefix and the stencil_slab_* signatures
+// (tests/cpu_slab/binding.py maps them onto stencil_amd.engine.SlabJob).
+// Never linked into the product: it links liboracle.so.
+#include <chrono>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "oracle.h"
+#include "slab_core.hpp"
+
+namespace stencil {
+
+namespace {
+thread_local int g_code = STENCIL_OK;
+thread_local char g_msg[512] = "";
+}  // namespace
+
+int set_error(int code, const char* fmt, ...) {
+    g_code = code;
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(g_msg, sizeof g_msg, fmt, ap);
+    va_end(ap);
+    return code;
+}
+void clear_error() {
+    g_code = STENCIL_OK;
+    g_msg[0] = '\0';
+}
+
+namespace fake {
+
+int g_k = 0;                          // sweeps per round (0: the library's rule)
+bool g_signal = true;                 // face-signalled rounds allowed
+int64_t g_free = int64_t(1) << 40;    // "device" free bytes (rolling margin from memory)
+std::mutex g_stat_mu;
+int64_t g_sweeps = 0, g_signal_sweeps = 0, g_sends = 0, g_recvs = 0, g_peer_copies = 0;
+
+struct Event {
+    std::chrono::steady_clock::time_point t{};
+};
+
+struct Mailbox {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::tuple<std::string, int, int>, std::deque<std::vector<char>>> q;
+    std::map<std::string, int> joined;  // rank-mode communicators per id
+};
+Mailbox& mailbox() {
+    static Mailbox m;
+    return m;
+}
+
+struct Comm {
+    std::string id;
+    int rank = 0, nranks = 1;
+};
+
+struct PendingRecv {
+    void* p;
+    size_t bytes;
+    int peer;
+    Comm* c;
+};
+thread_local int t_group = 0;
+thread_local std::vector<PendingRecv> t_pending;
+
+int take(void* p, size_t bytes, int peer, Comm* c) {
+    Mailbox& m = mailbox();
+    std::unique_lock<std::mutex> lk(m.mu);
+    const auto key = std::make_tuple(c->id, peer, c->rank);
+    if (!m.cv.wait_for(lk, std::chrono::seconds(20), [&] { return !m.q[key].empty(); }))
+        return set_error(STENCIL_EHIP, "fake recv: rank %d waited 20 s for rank %d", c->rank, peer);
+    std::vector<char> msg = std::move(m.q[key].front());
+    m.q[key].pop_front();
+    if (msg.size() != bytes)
+        return set_error(STENCIL_EHIP, "fake recv: %zu bytes posted, %zu sent", bytes, msg.size());
+    std::memcpy(p, msg.data(), bytes);
+    return STENCIL_OK;
+}
+
+}  // namespace fake
+
+struct FakeDev {
+    using Stream = void*;
+    using Event = fake::Event*;
+    using Comm = fake::Comm*;
+
+    static int set_device(int) { return STENCIL_OK; }
+    // api.hip's stencil_layout_init arithmetic (the rows padded so interior
+    // x = 0 sits on a 128-B boundary)
+    static int layout_init(const stencil_problem* p, stencil_layout* out) {
+        if (!p || p->dims != 3 || p->radius < 1 || p->nx < 0 || p->ny < 0 || p->nz < 0 ||
+            (p->halo > 0 && p->halo < p->radius))
+            return set_error(STENCIL_EINVAL, "fake layout: bad problem");
+        const int64_t r = p->radius, es = p->dtype == STENCIL_F32 ? 4 : 8;
+        const int64_t align = 128 / es;
+        const int64_t origin_x = (r + align - 1) / align * align;
+        stencil_layout l{};
+        l.prob = *p;
+        l.row = (origin_x + p->nx + r + align - 1) / align * align;
+        l.rows = p->ny + 2 * r;
+        l.plane = l.row * l.rows;
+        l.zghost = std::max<int64_t>(r, p->halo);
+        l.planes = p->nz + 2 * l.zghost;
+        l.origin = l.zghost * l.plane + r * l.row + origin_x;
+        l.elems = l.plane * l.planes;
+        l.bytes = l.elems * es;
+        *out = l;
+        return STENCIL_OK;
+    }
+    // iterate_tk_steps / iterate_box_steps of api.hip, unless a test sets K
+    static int fuse_depth(const stencil_problem& p) {
+        if (fake::g_k > 0) return fake::g_k;
+        if (p.shape == STENCIL_BOX) return p.nx * p.ny >= int64_t(384) * 384 ? 4 : 3;
+        return p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4;
+    }
+    static bool signal_enabled() { return fake::g_signal; }
+    static int free_bytes(int64_t* out) {
+        *out = fake::g_free;
+        return STENCIL_OK;
+    }
+    static int alloc(int64_t bytes, void** p) {
+        *p = std::calloc(size_t(bytes), 1);
+        return *p ? STENCIL_OK : set_error(STENCIL_ENOMEM, "fake alloc of %lld bytes", (long long)bytes);
+    }
+    static void free(void* p) { std::free(p); }
+    static int alloc_counters(uint32_t** c) {
+        *c = static_cast<uint32_t*>(std::calloc(4, sizeof(uint32_t)));
+        return *c ? STENCIL_OK : set_error(STENCIL_ENOMEM, "fake counters");
+    }
+    static void free_counters(uint32_t* c) { std::free(c); }
+    static int stream_create(Stream* s, bool) {
+        static char dummy;
+        *s = &dummy;
+        return STENCIL_OK;
+    }
+    static void stream_destroy(Stream) {}
+    static int stream_sync(Stream) { return STENCIL_OK; }
+    static int event_create(Event* e, bool) {
+        *e = new fake::Event;
+        return STENCIL_OK;
+    }
+    static void event_destroy(Event e) { delete e; }
+    static int event_record(Event e, Stream) {
+        e->t = std::chrono::steady_clock::now();
+        return STENCIL_OK;
+    }
+    static int stream_wait(Stream, Event) { return STENCIL_OK; }
+    static int event_elapsed(float* ms, Event a, Event b) {
+        *ms = std::chrono::duration<float, std::milli>(b->t - a->t).count();
+        return STENCIL_OK;
+    }
+
+    // ---- the sweep: stencil_sweepk's contract through the oracle
+    template <typename T>
+    static int sweep_t(const stencil_layout* l, const T* src, T* dst, int64_t b, int64_t e, int k) {
+        const stencil_problem& p = l->prob;
+        const int64_t r = p.radius, zg = l->zghost, n = p.nz;
+        const int64_t lo_bound = (p.flags & STENCIL_HALO_LO) ? -zg : -r;
+        const int64_t hi_bound = (p.flags & STENCIL_HALO_HI) ? n + zg : n + r;
+        const int64_t zlo = std::max(b - int64_t(k) * r, lo_bound), zhi = std::min(e + int64_t(k) * r, hi_bound);
+        oracle_problem op{};
+        op.dims = 3;
+        op.dtype = p.dtype == STENCIL_F64 ? ORACLE_F64 : ORACLE_F32;
+        op.shape = p.shape == STENCIL_BOX ? ORACLE_BOX : ORACLE_STAR;
+        op.radius = int32_t(r);
+        op.order = ORACLE_ORDER_NAIVE;
+        op.nx = p.nx;
+        op.ny = p.ny;
+        op.nz = (zhi - zlo) - 2 * r;
+        if (op.nz < e - b) return set_error(STENCIL_EINVAL, "fake sweep: range [%lld, %lld) beyond the readable planes",
+                                           (long long)b, (long long)e);
+        const int64_t sx = p.nx + 2 * r, sy = p.ny + 2 * r;
+        std::vector<T> A(size_t(sx * sy * (zhi - zlo))), B;
+        for (int64_t z = zlo; z < zhi; ++z)
+            for (int64_t y = -r; y < p.ny + r; ++y)
+                std::memcpy(&A[size_t(((z - zlo) * sy + (y + r)) * sx)], src + l->origin + z * l->plane + y * l->row - r,
+                            size_t(sx) * sizeof(T));
+        B = A;
+        const int in_b = oracle_run(&op, uint32_t(k), A.data(), B.data(), 1);
+        if (in_b < 0) return set_error(STENCIL_EINVAL, "fake sweep: oracle error %d", in_b);
+        const std::vector<T>& R = in_b ? B : A;
+        for (int64_t z = b; z < e; ++z)
+            for (int64_t y = 0; y < p.ny; ++y)
+                std::memcpy(dst + l->origin + z * l->plane + y * l->row, &R[size_t(((z - zlo) * sy + (y + r)) * sx + r)],
+                            size_t(p.nx) * sizeof(T));
+        return STENCIL_OK;
+    }
+    static int sweepk(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k, Stream) {
+        if (b < 0 || e > l->prob.nz || b > e || k < 1) return set_error(STENCIL_EINVAL, "fake sweep: bad range");
+        {
+            std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+            ++fake::g_sweeps;
+        }
+        if (b == e) return STENCIL_OK;
+        return l->prob.dtype == STENCIL_F64
+                   ? sweep_t(l, static_cast<const double*>(src), static_cast<double*>(dst), b, e, k)
+                   : sweep_t(l, static_cast<const float*>(src), static_cast<float*>(dst), b, e, k);
+    }
+    static int sweepk_signal(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k,
+                             uint32_t* counters, int* nsig, Stream s) {
+        if (int rc = sweepk(l, src, dst, b, e, k, s)) return rc;
+        {
+            std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+            ++fake::g_signal_sweeps;
+        }
+        counters[0] += 1;  // one add per face and launch (the faces are stored)
+        counters[1] += 1;
+        *nsig = 1;
+        return STENCIL_OK;
+    }
+    static int wait_counters(uint32_t* c, uint32_t lo, uint32_t hi, Stream) {
+        if (c[0] < lo || c[1] < hi) c[2] = 1;  // synchronous: a count short now never arrives
+        return STENCIL_OK;
+    }
+    static int read_timeout(uint32_t* c, bool* timed_out) {
+        *timed_out = c[2] != 0;
+        return STENCIL_OK;
+    }
+    static int copy_d2d(void* dst, const void* src, size_t bytes, Stream) {
+        std::memmove(dst, src, bytes);
+        return STENCIL_OK;
+    }
+    static int copy_peer(void* dst, int, const void* src, int, size_t bytes, Stream) {
+        std::memmove(dst, src, bytes);
+        std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+        ++fake::g_peer_copies;
+        return STENCIL_OK;
+    }
+    // api.hip's fill_initial_kernel: padding 0, x-ghosts 1 at every y and z,
+    // interior 0 or splitmix64(seed + linear index) (the oracle's u01)
+    template <typename T>
+    static void fill_t(const stencil_layout* l, T* g, int kind, uint64_t seed) {
+        const stencil_problem& p = l->prob;
+        const int64_t r = p.radius, ox = l->origin % l->row;
+        for (int64_t pz = 0; pz < l->planes; ++pz)
+            for (int64_t py = 0; py < l->rows; ++py)
+                for (int64_t px = 0; px < l->row; ++px) {
+                    const int64_t x = px - ox, y = py - r, z = pz - l->zghost;
+                    T v = T(0);
+                    if (x >= -r && x < p.nx + r) {
+                        const bool xghost = x < 0 || x >= p.nx;
+                        const bool interior = !xghost && y >= 0 && y < p.ny && z >= 0 && z < p.nz;
+                        if (xghost) {
+                            v = T(1);
+                        } else if (interior && kind == STENCIL_INIT_RANDOM) {
+                            uint64_t u = seed + uint64_t((z * p.ny + y) * p.nx + x);
+                            u += 0x9e3779b97f4a7c15ULL;
+                            u = (u ^ (u >> 30)) * 0xbf58476d1ce4e5b9ULL;
+                            u = (u ^ (u >> 27)) * 0x94d049bb133111ebULL;
+                            u ^= u >> 31;
+                            v = sizeof(T) == 4 ? T(float(u >> 40) * 0x1.0p-24f) : T(double(u >> 11) * 0x1.0p-53);
+                        }
+                    }
+                    g[(pz * l->rows + py) * l->row + px] = v;
+                }
+    }
+    static int fill_initial(const stencil_layout* l, void* g, int kind, uint64_t seed, Stream) {
+        if (l->prob.dtype == STENCIL_F64)
+            fill_t(l, static_cast<double*>(g), kind, seed);
+        else
+            fill_t(l, static_cast<float*>(g), kind, seed);
+        return STENCIL_OK;
+    }
+    // api.hip's copy_grid: host planes z = -r .. nz+r-1, x/y ghosts included
+    static int copy_grid(const stencil_layout* l, void* g, const void* hs, void* hd, int64_t row, int64_t rows) {
+        const stencil_problem& p = l->prob;
+        const int64_t r = p.radius;
+        const size_t es = p.dtype == STENCIL_F64 ? 8 : 4;
+        const int64_t width = p.nx + 2 * r, height = p.ny + 2 * r;
+        if (row < width || rows < height) return set_error(STENCIL_EINVAL, "host array too small");
+        for (int64_t hz = 0; hz < p.nz + 2 * r; ++hz)
+            for (int64_t y = 0; y < height; ++y) {
+                char* d = static_cast<char*>(g) + size_t(l->origin + (hz - r) * l->plane + (y - r) * l->row - r) * es;
+                const size_t h = size_t((hz * rows + y) * row) * es;
+                if (hs)
+                    std::memcpy(d, static_cast<const char*>(hs) + h, size_t(width) * es);
+                else
+                    std::memcpy(static_cast<char*>(hd) + h, d, size_t(width) * es);
+            }
+        return STENCIL_OK;
+    }
+    static int upload(const stencil_layout* l, void* g, const void* h, int64_t row, int64_t rows, Stream) {
+        return copy_grid(l, g, h, nullptr, row, rows);
+    }
+    static int download(const stencil_layout* l, const void* g, void* h, int64_t row, int64_t rows, Stream) {
+        return copy_grid(l, const_cast<void*>(g), nullptr, h, row, rows);
+    }
+    static int plane_sums(const stencil_layout* l, const void* g, double* out, Stream) {
+        const stencil_problem& p = l->prob;
+        for (int64_t z = 0; z < p.nz; ++z) {
+            double acc = 0;
+            for (int64_t y = 0; y < p.ny; ++y)
+                for (int64_t x = 0; x < p.nx; ++x) {
+                    const int64_t i = l->origin + z * l->plane + y * l->row + x;
+                    acc += p.dtype == STENCIL_F64 ? static_cast<const double*>(g)[i]
+                                                  : double(static_cast<const float*>(g)[i]);
+                }
+            out[z] = acc;
+        }
+        return STENCIL_OK;
+    }
+
+    // ---- the communicator
+    static bool comm_available() { return true; }
+    static int comm_init_all(Comm* comms, int n, const int*) {
+        std::random_device rd;
+        const std::string id = "all:" + std::to_string(rd()) + ":" + std::to_string(rd());
+        for (int i = 0; i < n; ++i) comms[i] = new fake::Comm{id, i, n};
+        return STENCIL_OK;
+    }
+    static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank) {
+        const std::string key(static_cast<const char*>(id), STENCIL_SLAB_ID_BYTES);
+        fake::Mailbox& m = fake::mailbox();
+        std::unique_lock<std::mutex> lk(m.mu);
+        ++m.joined[key];
+        m.cv.notify_all();
+        // a collective, as ncclCommInitRank: every rank of the id must arrive
+        if (!m.cv.wait_for(lk, std::chrono::seconds(20), [&] { return m.joined[key] >= nranks; }))
+            return set_error(STENCIL_EHIP, "fake comm init: %d of %d ranks joined", m.joined[key], nranks);
+        *comm = new fake::Comm{key, rank, nranks};
+        return STENCIL_OK;
+    }
+    static void comm_destroy(Comm c) { delete c; }
+    static int group_start() {
+        ++fake::t_group;
+        return STENCIL_OK;
+    }
+    static int group_end() {
+        if (fake::t_group <= 0) return set_error(STENCIL_EINVAL, "fake group_end without group_start");
+        if (--fake::t_group > 0) return STENCIL_OK;
+        std::vector<fake::PendingRecv> pend;
+        pend.swap(fake::t_pending);
+        for (const fake::PendingRecv& r : pend)
+            if (int rc = fake::take(r.p, r.bytes, r.peer, r.c)) return rc;
+        return STENCIL_OK;
+    }
+    static int send(const void* p, size_t bytes, int peer, Comm c, Stream) {
+        if (peer < 0 || peer >= c->nranks) return set_error(STENCIL_EINVAL, "fake send to rank %d of %d", peer, c->nranks);
+        fake::Mailbox& m = fake::mailbox();
+        {
+            std::lock_guard<std::mutex> lk(m.mu);
+            m.q[std::make_tuple(c->id, c->rank, peer)].emplace_back(static_cast<const char*>(p),
+                                                                    static_cast<const char*>(p) + bytes);
+        }
+        m.cv.notify_all();
+        std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+        ++fake::g_sends;
+        return STENCIL_OK;
+    }
+    static int recv(void* p, size_t bytes, int peer, Comm c, Stream) {
+        if (peer < 0 || peer >= c->nranks) return set_error(STENCIL_EINVAL, "fake recv from rank %d of %d", peer, c->nranks);
+        {
+            std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+            ++fake::g_recvs;
+        }
+        if (fake::t_group > 0) {
+            fake::t_pending.push_back({p, bytes, peer, c});
+            return STENCIL_OK;
+        }
+        return fake::take(p, bytes, peer, c);
+    }
+};
+
+}  // namespace stencil
+
+struct fake_slab_job : stencil::slab::Job<stencil::FakeDev> {};
+
+using stencil::FakeDev;
+namespace core = stencil::slab;
+
+extern "C" {
+
+const char* fake_slab_last_error_message(void) { return stencil::g_msg; }
+void fake_slab_set_k(int32_t k) { stencil::fake::g_k = k; }
+void fake_slab_set_signal(int32_t on) { stencil::fake::g_signal = on != 0; }
+void fake_slab_set_free_bytes(int64_t b) { stencil::fake::g_free = b; }
+// sweeps, face-signalled sweeps, sends, receives, peer copies since the last reset
+void fake_slab_stats(int64_t* out5, int32_t reset) {
+    std::lock_guard<std::mutex> lk(stencil::fake::g_stat_mu);
+    using namespace stencil::fake;
+    if (out5) {
+        out5[0] = g_sweeps;
+        out5[1] = g_signal_sweeps;
+        out5[2] = g_sends;
+        out5[3] = g_recvs;
+        out5[4] = g_peer_copies;
+    }
+    if (reset) g_sweeps = g_signal_sweeps = g_sends = g_recvs = g_peer_copies = 0;
+}
+
+int fake_slab_create(const stencil_problem* g, int32_t n, const int32_t* devs, int32_t ex, int32_t flags,
+                     fake_slab_job** job) {
+    return core::create<FakeDev>(g, n, devs, ex, flags, 0, job);
+}
+int fake_slab_create2(const stencil_problem* g, int32_t n, const int32_t* devs, int32_t ex, int32_t flags,
+                      int64_t margin, fake_slab_job** job) {
+    return core::create<FakeDev>(g, n, devs, ex, flags, margin, job);
+}
+int fake_slab_unique_id(void* id, int64_t bytes) {
+    if (!id || bytes < STENCIL_SLAB_ID_BYTES) return stencil::set_error(STENCIL_EINVAL, "id buffer too small");
+    std::random_device rd;
+    std::memset(id, 0, size_t(STENCIL_SLAB_ID_BYTES));
+    std::snprintf(static_cast<char*>(id), size_t(STENCIL_SLAB_ID_BYTES), "rank:%u:%u:%u", rd(), rd(), rd());
+    return STENCIL_OK;
+}
+int fake_slab_create_rank(const stencil_problem* g, int32_t nranks, int32_t rank, int32_t dev, const void* id,
+                          int64_t id_bytes, int32_t flags, fake_slab_job** job) {
+    return core::create_rank<FakeDev>(g, nranks, rank, dev, id, id_bytes, flags, 0, job);
+}
+int fake_slab_create_rank2(const stencil_problem* g, int32_t nranks, int32_t rank, int32_t dev, const void* id,
+                           int64_t id_bytes, int32_t flags, int64_t margin, fake_slab_job** job) {
+    return core::create_rank<FakeDev>(g, nranks, rank, dev, id, id_bytes, flags, margin, job);
+}
+int fake_slab_destroy(fake_slab_job* job) {
+    core::release<FakeDev>(job);
+    return STENCIL_OK;
+}
+int fake_slab_info(const fake_slab_job* job, int32_t slab, int64_t* first, int64_t* planes, int32_t* dev, int32_t* k) {
+    return core::info<FakeDev>(job, slab, first, planes, dev, k);
+}
+int fake_slab_rolling_info(const fake_slab_job* job, int64_t* margin, int64_t* launches) {
+    return core::rolling_info<FakeDev>(job, margin, launches);
+}
+int fake_slab_fill_initial(fake_slab_job* job, int32_t kind, uint64_t seed) {
+    return core::fill_initial<FakeDev>(job, kind, seed);
+}
+int fake_slab_upload(fake_slab_job* job, const void* host, int64_t row, int64_t rows) {
+    return core::upload<FakeDev>(job, host, row, rows);
+}
+int fake_slab_download(fake_slab_job* job, void* host, int64_t row, int64_t rows) {
+    return core::download<FakeDev>(job, host, row, rows);
+}
+int fake_slab_run(fake_slab_job* job, uint32_t iterations, float* ms) { return core::run<FakeDev>(job, iterations, ms); }
+int fake_slab_kernel_timing(fake_slab_job* job, int32_t enable) { return core::kernel_timing<FakeDev>(job, enable); }
+int fake_slab_kernel_time(fake_slab_job* job, float* ms, int64_t* n, int64_t* cells, int32_t* sig) {
+    return core::kernel_time<FakeDev>(job, ms, n, cells, sig);
+}
+int fake_slab_plane_sums(fake_slab_job* job, double* sums) { return core::plane_sums<FakeDev>(job, sums); }
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+"""The multi-GPU slab job's round logic on the CPU.
+
+csrc/slab_core.hpp holds the z-slab job -- the z split, the three round forms
+(boundary + interior launches, face-signalled launches, rolling one-grid
+passes), the halo exchange and its posting order, the remainder rounds, the
+ghost-plane restores -- once, over a device backend.  The product binds it to
+HIP and RCCL (csrc/slab.hip); tests/cpu_slab/fake_dev.cpp binds it to a CPU
+fake device whose sweeps are the oracle's and whose communicator is an
+in-process mailbox.  So the code that runs on the 8-GPU node runs here, at
+world 2 and 3 (single-process jobs and rank-mode jobs, one thread per rank),
+checked bit for bit against ONE grid swept by the oracle.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+from stencil_amd import _lib
+from stencil_amd.engine import SlabJob, StencilSpec
+from tests.cpu_slab import binding as fb
+
+pytestmark = pytest.mark.skipif(not fb.available(), reason="tests/cpu_slab/libslab_fake.so not built (run make)")
+
+
+@pytest.fixture()
+def fake():
+    lib = fb.load()
+    lib.set_k(0)
+    lib.set_signal(True)
+    lib.set_free_bytes(1 << 40)
+    yield lib
+    lib.set_k(0)
+    lib.set_signal(True)
+    lib.set_free_bytes(1 << 40)
+
+
+def oracle_grid(spec, nx, ny, nz, sweeps, kind="random", seed=11):
+    p = ob.problem(3, spec.dtype, spec.shape, spec.radius, "naive", nx, ny, nz)
+    return ob.run(p, sweeps, kind, seed)
+
+
+def assert_bitwise(got, want):
+    assert got.shape == want.shape
+    if not np.array_equal(got.view(np.uint8), want.view(np.uint8)):
+        diff = np.argwhere(got != want)
+        raise AssertionError(f"{len(diff)} cells differ, first at {diff[:4].tolist()}")
+
+
+SHAPES = [
+    ("fp64", "star", 4),
+    ("fp32", "star", 5),
+    ("fp64", "box", 4),
+    ("fp32", "box", 3),
+]
+
+
+@pytest.mark.parametrize("dtype,shape,k", SHAPES)
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("exchange,devices", [("rccl", "distinct"), ("copy", "distinct"), ("copy", "shared")])
+def test_single_process_job_equals_one_grid(fake, dtype, shape, k, nslabs, exchange, devices):
+    """N slabs from one process (stencil_slab_create), every round form the
+    device assignment selects: distinct devices -> face-signalled full rounds,
+    shared -> boundary + interior launches; remainder rounds; bitwise."""
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz = 13, 7, 3 * k * nslabs + 2  # remainder planes to the lowest slabs
+    devs = list(range(nslabs)) if devices == "distinct" else [0] * nslabs
+    job = SlabJob(spec, nx, ny, nz, devs, exchange=exchange, lib=fake)
+    job.fill_initial("random", 11)
+    sweeps = 0
+    for it in (2 * k + 1, k, 1, k - 1):  # full + remainder rounds, continued calls
+        fake.stats(reset=True)
+        job.run(it)
+        sweeps += it
+        st = fake.stats()
+        full = it // k
+        signalled = len(set(devs)) == len(devs)
+        assert st["signal_sweeps"] == (full * nslabs if signalled else 0), st
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps))
+    job.close()
+
+
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("exchange", ["rccl", "copy"])
+def test_periodic_ring_equals_replicated_grid(fake, nslabs, exchange):
+    """PERIODIC joins the z ends (the self-ring rehearsal of an interior
+    rank): equal to the middle third of a grid of three copies swept by the
+    oracle, for fewer sweeps than one copy's planes."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 9, 6, 10 * nslabs
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange=exchange, periodic=True, lib=fake)
+    p1 = ob.problem(3, "fp64", "star", 1, "naive", nx, ny, nz)
+    g0 = ob.init(p1, "random", 5)
+    job.upload(g0)
+    sweeps = 9
+    job.run(sweeps)
+    got = job.download()
+    p3 = ob.problem(3, "fp64", "star", 1, "naive", nx, ny, 3 * nz)
+    g3 = ob.init(p3, "reference")
+    inner = g0[1:nz + 1]
+    g3[1:1 + 3 * nz] = np.concatenate([inner, inner, inner])
+    a, b = g3.copy(), g3.copy()
+    for _ in range(sweeps):
+        ob.sweep(p3, a, b, 0, 3 * nz)
+        a, b = b, a
+    assert_bitwise(got[1:nz + 1], a[1 + nz:1 + 2 * nz])
+    job.close()
+
+
+@pytest.mark.parametrize("dtype,shape,k", [("fp64", "star", 4), ("fp32", "box", 3)])
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("margin_extra", [1, 3, 40])
+def test_rolling_slabs_equal_one_grid(fake, dtype, shape, k, nslabs, margin_extra):
+    """ROLLING: one resident grid per slab plus a margin -- from one-plane
+    launches (margin = K r + 1) to one launch per pass; down and up passes,
+    remainder passes, the halo exchange after each pass and the global ends'
+    ghost restores; bitwise the oracle's one grid."""
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz = 11, 5, 7 * nslabs + 1
+    margin = k + margin_extra
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange="rccl", rolling=True, margin=margin, lib=fake)
+    info = job.rolling_info()
+    assert info["margin"] == margin
+    assert info["launches_per_pass"] == -(-(nz // nslabs + (1 if nz % nslabs else 0)) // margin_extra)
+    job.fill_initial("random", 3)
+    sweeps = 0
+    for it in (k, 2 * k + 2, 1):  # a down pass, up + down + a 2-sweep remainder pass, a single
+        fake.stats(reset=True)
+        job.run(it)
+        sweeps += it
+        assert fake.stats()["signal_sweeps"] == 0  # rolling rounds are plain passes
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps, seed=3))
+    job.kernel_timing(True)
+    job.run(k)
+    kt = job.kernel_time()
+    assert kt["rolling"] and not kt["signalled"] and kt["launches"] == 1 and kt["cells_per_launch"] > 0
+    job.close()
+
+
+def test_rolling_margin_from_free_memory(fake):
+    """margin 0 sizes the margin from the device's free memory (capped at 512
+    planes; refused when even 4 (K r + 1) planes do not fit)."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 16, 16, 40, [0, 1], exchange="rccl", rolling=True, margin=0, lib=fake)
+    assert job.rolling_info()["margin"] == 512
+    job.close()
+    fake.set_free_bytes(4 << 30)  # the communicator's reserve and nothing beside it
+    with pytest.raises(_lib.StencilError, match="do not fit"):
+        SlabJob(spec, 16, 16, 40, [0, 1], exchange="rccl", rolling=True, margin=0, lib=fake)
+
+
+def _rank_jobs(fake, spec, grid, nranks, fn, rolling=False, margin=0):
+    """Run `fn(job, rank)` for a rank-mode job in one thread per rank (ctypes
+    releases the GIL: the ranks' blocking receives overlap like processes)."""
+    uid = SlabJob.unique_id(lib=fake)
+    out, errs = [None] * nranks, [None] * nranks
+
+    def body(r):
+        try:
+            job = SlabJob(spec, *grid, [r], rank=(nranks, r, uid), rolling=rolling, margin=margin, lib=fake)
+            out[r] = fn(job, r)
+            job.close()
+        except Exception as exc:  # surfaced below
+            errs[r] = exc
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    return out, errs
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("rolling", [False, True])
+@pytest.mark.parametrize("shape", ["star", "box"])
+def test_rank_mode_equals_one_grid(fake, nranks, rolling, shape):
+    """Rank mode (stencil_slab_create_rank: one slab per process, peers by
+    global index, as torch.distributed.run launches bench.py on the 8-GPU
+    node), one thread per rank: each rank's planes, assembled, bitwise the
+    oracle's one grid; face-signalled rounds when not rolling."""
+    k = 4 if shape == "star" else 3
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype="fp64", shape=shape)
+    nx, ny, nz = 10, 6, 9 * nranks + 1
+    sweeps = 2 * k + 3
+
+    def fn(job, r):
+        inf = job.info(0)
+        job.fill_initial("random", 21)
+        job.run(k + 1)
+        job.run(sweeps - k - 1)
+        return inf, job.download(), job.plane_sums()
+
+    out, errs = _rank_jobs(fake, spec, (nx, ny, nz), nranks, fn, rolling=rolling, margin=k + 2)
+    assert not any(errs), errs
+    want = oracle_grid(spec, nx, ny, nz, sweeps, seed=21)
+    got = np.zeros_like(want)
+    for r in range(nranks):
+        inf, dense, _ = out[r]
+        z0 = inf["first"] + (0 if r > 0 else -1)
+        z1 = inf["first"] + inf["planes"] + (1 if r == nranks - 1 else 0)
+        got[z0 + 1:z1 + 1] = dense[z0 + 1:z1 + 1]
+    assert_bitwise(got, want)
+
+
+def test_rank_mode_rejects_tiny_slabs_on_every_rank(fake):
+    """A job whose smallest slab is below the halo depth fails on EVERY rank
+    before the communicator's collective init (no rank left waiting in it)."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    out, errs = _rank_jobs(fake, spec, (8, 8, 11), 3, lambda job, r: None)  # 11 / 3 = 3 < 4 halo planes
+    assert all(isinstance(e, _lib.StencilError) and "use fewer GPUs" in str(e) for e in errs), errs
+
+
+def test_single_process_rejects_tiny_slabs(fake):
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    with pytest.raises(_lib.StencilError, match="use fewer GPUs"):
+        SlabJob(spec, 8, 8, 7, [0, 1], exchange="copy", lib=fake)
+
+
+def test_exchange_counts_per_round(fake):
+    """Per full round every shared face moves once each way: 2 (N - 1) sends
+    and receives for N slabs (a periodic ring: 2 N)."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    for periodic, n in ((False, 3), (True, 3), (True, 1)):
+        job = SlabJob(spec, 8, 8, 24, list(range(n)), exchange="rccl", periodic=periodic, lib=fake)
+        job.fill_initial("reference")
+        fake.stats(reset=True)
+        job.run(8)  # two full rounds
+        st = fake.stats()
+        faces = 2 * n if periodic else 2 * (n - 1)
+        assert st["sends"] == st["recvs"] == 2 * faces, (periodic, n, st)
+        job.close()
