@@ -1,40 +1,46 @@
 #!/usr/bin/env python3
 """Benchmark: 3D 7-point fp64 Jacobi (BASELINE.json metric, config 2 size per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|NS]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4|C5|NS|NS4096]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
-
-Multi-GPU drivers, same job, same JSON line:
-  * one process per GPU (launched by torch.distributed.run; WORLD_SIZE set):
-    the C-ABI rank-mode slab job (stencil_slab_create_rank: each rank its own
-    slab, RCCL between the ranks); --driver python (or a rehearsal transport)
-    runs stencil_amd/slab.py over torch.distributed instead;
-  * --gpus N without a launcher (WORLD_SIZE unset): ONE process drives the N
-    GPUs through the C-ABI slab job (stencil_slab_*, csrc/slab.hip; RCCL
-    ncclCommInitAll), the shape of the reference's single spawn/join of its
-    whole decomposed job (src/stencil/stencil.cpp:34-53).
-
---config picks another BASELINE.json config as the workload (C3: 4096^3 fp32,
-C4: 2048x2048x4096 fp64, C5: 2048^3 27-point fp64), its global grid z-slab
-split over the N ranks; the default C2 is the metric's own config.
 
 One step = one Jacobi sweep of the whole grid.  At N=1 the workload is
 BASELINE config 2 (512^3 interior, fp64, 7-point star; the default K=1000 is
 exactly its 1000 iterations).  At N>1 every rank owns a 512^3 Z-slab of a
 512 x 512 x 512N grid (weak scaling) and exchanges K halo planes with each
 neighbour per round of K fused sweeps (K = 4: the strip-layout K-step
-kernel) over RCCL, the boundary planes' launch and the send/recv overlapped
-with the interior launch on a second stream.
+kernel) over RCCL, overlapped with the rest of the round's launch
+(face-signalled rounds, csrc/slab_core.hpp).
+
+Multi-GPU drivers, same job, same JSON line, ONE implementation of the rounds
+(the C-ABI slab job, csrc/slab_core.hpp):
+  * one process per GPU (launched by torch.distributed.run; WORLD_SIZE set):
+    rank mode (stencil_slab_create_rank: each rank its own slab, RCCL between
+    the ranks); torch.distributed (gloo, host side only) carries the RCCL id,
+    the barriers, the max-over-ranks time and the check's per-plane sums;
+  * --gpus N without a launcher (WORLD_SIZE unset): ONE process drives the N
+    GPUs (stencil_slab_create; RCCL ncclCommInitAll), the shape of the
+    reference's single spawn/join of its whole decomposed job
+    (src/stencil/stencil.cpp:34-53);
+  * --exchange loopback | nccl-self at N=1: one slab whose z ends form a ring
+    (periodic), halos by device copies or RCCL send/recv to itself -- the
+    interior-rank rehearsal on one GPU.
+
+--config picks another BASELINE.json config as the workload (C1: the
+reference's own 2D 1024^2 case; C3: 4096^3 fp32, C4: 2048x2048x4096 fp64, C5:
+2048^3 27-point fp64, their global grids z-slab split over the ranks; NS4096:
+the north star's own 4096^3 fp64 7-point grid, 2 GPUs or more).  Slabs whose
+two grids do not fit a GPU keep ONE grid plus a rolling margin
+(STENCIL_SLAB_ROLLING), as C3 / C4 do on one GPU.
 
 Rank 0 prints one JSON line with the whole-job rate, the live roofline of the
-dominant kernel (algorithmic bytes per launch / average launch time from HIP
+dominant kernel (compulsory bytes per launch / average launch time from HIP
 events on the kernel's own stream), and a bounded CPU baseline (the oracle's
-single-thread restatement of the reference's naive sweep, N=1 only).
+restatement of the reference's naive sweep, N=1 only).
 """
 from __future__ import annotations
 
 import argparse
-import dataclasses
 import json
 import os
 import sys
@@ -45,27 +51,36 @@ sys.path.insert(0, HERE)
 
 METRIC = "Gcell-updates/s + achieved HBM GB/s vs roofline, 7-pt fp64 Jacobi, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+GiB = 1 << 30
+# HBM kept free beside a slab's grids (RCCL's buffers and the library's scratch)
+SLAB_RESERVE = 8 * GiB
 
 
 # BASELINE.json configs as bench workloads.  C2 (the default, the metric's
-# config) is weak-scaled: n^3 per GPU.  C3-C5 are the configs' global grids,
+# config) is weak-scaled: n^3 per GPU.  C3-C5 and NS4096 are global grids,
 # z-slab split over the ranks (strong scaling); at N = 1, C3 and C4 keep ONE
-# resident grid (two would need 2 x 275 GB / 2 x 137 GB).
+# resident grid (two would need 2 x 279 GB / 2 x 138 GB).
 PRESETS = {
+    "C1": dict(dims=2, dtype="fp64", shape="star", grid=(1024, 1024, 1), min_gpus=1, max_gpus=1,
+               desc="BASELINE config 1: 2D 5-point fp64 Jacobi, 1024x1024 (the reference's own case, run.sh -s 1024)"),
     "C2": dict(dtype="fp64", shape="star", grid=None, min_gpus=1,
                desc="BASELINE config 2: 3D 7-point fp64 Jacobi, {n}^3 interior per GPU"),
     # C3 on one GPU: ONE resident grid + a rolling margin (stencil_rolling_*),
     # since two grids are 2 x 279 GB
     "C3": dict(dtype="fp32", shape="star", grid=(4096, 4096, 4096), min_gpus=1,
                desc="BASELINE config 3: 3D 7-point fp32 Jacobi, 4096^3"),
-    # C4 on one GPU likewise (one 137 GB grid + a margin)
+    # C4 on one GPU likewise (one 138 GB grid + a margin)
     "C4": dict(dtype="fp64", shape="star", grid=(2048, 2048, 4096), min_gpus=1,
                desc="BASELINE config 4: 3D 7-point fp64 Jacobi, 2048x2048x4096"),
     "C5": dict(dtype="fp64", shape="box", grid=(2048, 2048, 2048), min_gpus=1,
                desc="BASELINE config 5: 3D 27-point fp64 stencil, 2048^3, temporal blocking (4 sweeps per launch, "
                     "deeper than the config's 2; bitwise the same result)"),
-    # north_star's 4096^3 fp64 needs 2 x 550 GB; its largest single-GPU
-    # proxy is 2048^3 fp64: 2 x 70 GB with ghosts and padding
+    # north_star's own grid: 4096^3 fp64 is 550 GB per grid -- not even ONE
+    # grid fits a 288 GB MI355X; from 2 GPUs on (N = 2: one rolling 278 GB
+    # grid per GPU; N >= 4: two grids per slab)
+    "NS4096": dict(dtype="fp64", shape="star", grid=(4096, 4096, 4096), min_gpus=2,
+                   desc="north star: 3D 7-point fp64 Jacobi, 4096^3, z-slab split over the GPUs"),
+    # its largest single-GPU proxy: 2048^3 fp64, 2 x 70 GB
     "NS": dict(dtype="fp64", shape="star", grid=(2048, 2048, 2048), min_gpus=1,
                desc="north-star proxy: 3D 7-point fp64 Jacobi, 2048^3 (4096^3 does not fit one GPU)"),
 }
@@ -79,6 +94,7 @@ KERNEL_SOURCES = {
     "zmarch": ("stencil_amd/csrc/kernels_zmarch.hip",),
     "direct": ("stencil_amd/csrc/kernels_direct.hip",),
     "boxk": ("stencil_amd/csrc/kernels_boxk.hip",),
+    "tb2ds": ("stencil_amd/csrc/kernels_tb2d.hip",),
 }
 
 
@@ -91,28 +107,26 @@ def kernel_source_sha(kname: str):
     return h.hexdigest()[:16] if kname in KERNEL_SOURCES else None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(PRESETS),
-                    help="workload (default C2, the metric's config; C3-C5 split a global grid over the ranks)")
+                    help="workload (default C2, the metric's config; C3-C5 / NS4096 split a global grid over the ranks)")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
-    ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-signal", action="store_true",
-                    help="multi-GPU rounds as separate boundary/interior launches (no face counters)")
-    ap.add_argument("--face-signal", action="store_true",
-                    help="face-signalled rounds gated by hipStreamWaitValue64 on a signal word, not the wait kernel")
-    ap.add_argument("--exchange", default="nccl", choices=["nccl", "host", "loopback", "nccl-self", "copy"],
-                    help="halo transport: RCCL P2P (default) or host-staged gloo (single-GPU rehearsal only); "
-                         "without a launcher, copy = device copies between the slabs (hipMemcpyPeerAsync)")
+                    help="multi-GPU rounds as separate boundary/interior launches (no face counters; "
+                         "STENCIL_SLAB_SIGNAL=0)")
+    ap.add_argument("--exchange", default="nccl", choices=["nccl", "copy", "loopback", "nccl-self"],
+                    help="halo transport: RCCL P2P (default) or, without a launcher, device copies between the slabs "
+                         "(copy); at N=1, loopback / nccl-self rehearse an interior rank (a periodic slab whose "
+                         "halos are its own faces, by device copies / RCCL send-recv to itself)")
     ap.add_argument("--share-device", action="store_true",
-                    help="rehearsal: every rank / slab uses GPU 0 (needs --exchange host, or copy without a launcher)")
-    ap.add_argument("--driver", default="auto", choices=["auto", "cabi", "python"],
-                    help="under torch.distributed.run: the C-ABI rank-mode slab job (auto/cabi) or the Python slab "
-                         "driver over torch.distributed (python; auto picks it for the rehearsal transports)")
+                    help="rehearsal without a launcher: every slab on GPU 0 (needs --exchange copy)")
+    ap.add_argument("--rolling", choices=["auto", "on", "off"], default="auto",
+                    help="slabs: ONE grid + a rolling margin (on), two grids (off), or whatever fits (auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
@@ -120,12 +134,14 @@ def parse():
     ap.add_argument("--allow-debug-library", action="store_true",
                     help="bench even when an experiment knob (a STENCIL_* variable the product ignores) is set, "
                          "i.e. on libstencil_hip_debug.so; the JSON line names the library and the knobs either way")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     from stencil_amd import _lib
     if _lib.debug_knobs_requested() and not args.allow_debug_library:
         knobs = sorted(k for k in os.environ if k.startswith("STENCIL_") and k not in _lib.API_KNOBS)
         raise SystemExit(f"experiment knobs set ({', '.join(knobs)}): this would bench libstencil_hip_debug.so; "
                          "unset them or pass --allow-debug-library")
+    if args.no_signal:
+        os.environ["STENCIL_SLAB_SIGNAL"] = "0"  # an API knob: read at slab creation
     return args
 
 
@@ -149,23 +165,25 @@ def host_threads() -> int:
     return max(1, min(n, int(env))) if env.isdigit() and int(env) > 0 else n
 
 
-def cpu_baseline(n: int, budget_s: float, threads: int = 1, dtype: str = "fp64", shape: str = "star"):
+def cpu_baseline(n: int, budget_s: float, threads: int = 1, dtype: str = "fp64", shape: str = "star", dims: int = 3,
+                 iters_cap: int = 200):
     """The oracle (port of check_result's loop, stencil.cpp:94-131, generalised
-    to 3D) on the host over a bounded number of sweeps of an n^3 grid of the
+    to 3D) on the host over a bounded number of sweeps of an n^dims grid of the
     workload's stencil: single-threaded like the reference's own CPU path, or
     with OpenMP over `threads` cores (identical per-cell arithmetic,
     bitwise-equal result)."""
     from oracle import binding as ob
-    p = ob.problem(3, dtype, shape, 1, "naive", n, n, n)
+    p = ob.problem(dims, dtype, shape, 1, "naive", n, n, n if dims == 3 else 1)
     t1 = ob.timed_run(p, 1, threads=threads)
-    iters = max(1, min(200, int(budget_s / max(t1, 1e-6))))
+    iters = max(1, min(iters_cap, int(budget_s / max(t1, 1e-6))))
     t = ob.timed_run(p, iters, threads=threads)
-    cells = float(n) ** 3 * iters
+    cells = float(n) ** dims * iters
     who = "1 host thread" if threads == 1 else f"{threads} host threads (OpenMP)"
-    pts = "7-point" if shape == "star" else "27-point"
+    pts = {(3, "star"): "7-point", (3, "box"): "27-point", (2, "star"): "5-point"}[(dims, shape)]
+    shape_s = f"{n}^{dims}"
     return {"value": round(cells / t / 1e9, 4), "unit": "Gcell-updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ naive sweep, {n}^3 {dtype} {pts}, {iters} sweeps from the reference initial "
-                      f"condition, {t:.1f} s on {who}"}
+            "sample": f"oracle/ naive sweep, {shape_s} {dtype} {pts}, {iters} sweeps from the reference initial "
+                      f"condition, {t:.2f} s on {who}"}
 
 
 def load_traffic(workload_key: str, kernel_name: str):
@@ -184,269 +202,76 @@ def load_traffic(workload_key: str, kernel_name: str):
     return (ent.get("hbm_bytes_per_launch") if fresh else None), dict(ent, fresh=fresh)
 
 
-def verify_slabs(eng, slab, spec, grid, world, rank, sweeps, on_gpu, local):
-    """End-to-end check of a multi-GPU run, after the timed region: every
-    rank's per-plane sums (fp64, one deterministic sum per plane) gathered on
-    rank 0 and compared BIT FOR BIT with the same number of sweeps of the
-    whole global grid run as ONE grid on rank 0's GPU -- the slabs' exchange,
-    fused rounds and face signalling must not change a single bit (SURVEY
-    8(e)).  Skipped when the global grid does not fit beside rank 0's slab."""
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
-    from stencil_amd.engine import JacobiEngine
-    from stencil_amd.slab import partition
-
-    gnx, gny, gnz = grid
-    counts = [partition(gnz, world, r)[1] for r in range(world)]
-    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
-    buf = torch.zeros(max(counts), dtype=torch.float64)
-    buf[:counts[rank]] = torch.from_numpy(eng.plane_sums(slab.cur))
-    buf = buf.to(dev)
-    parts = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf)
-    result = None
-    if rank == 0:
-        try:
-            got = np.concatenate([parts[r].cpu().numpy()[:counts[r]] for r in range(world)])
-            need = 2.2 * gnx * gny * gnz * spec.elem_bytes  # two padded grids
-            free = torch.cuda.mem_get_info(local)[0]
-            if need > 0.9 * free:
-                result = {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free"}
-            else:
-                ref = JacobiEngine(dataclasses.replace(spec, halo=0), gnx, gny, gnz, device=local)
-                ref.reset("reference")
-                fin, _ = ref.iterate(sweeps)
-                want = ref.plane_sums(fin)
-                bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
-                result = {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad,
-                          "bitwise_equal": bad == 0,
-                          "reference": "the global grid as one grid on rank 0's GPU, same sweeps, per-plane sums"}
-                del ref, fin
-                torch.cuda.empty_cache()
-        except Exception as exc:  # a check, never the measurement
-            result = {"error": f"{type(exc).__name__}: {exc}"[:300]}
-    dist.barrier()
-    return result
+# ----------------------------------------------------------------- planning
+def partition(nz: int, world: int, rank: int):
+    """Contiguous z-slab `rank` of `world`: (first plane, planes); the nz %
+    world remainder planes go to the lowest ranks (csrc/slab_core.hpp's split)."""
+    base, rem = divmod(nz, world)
+    return rank * base + min(rank, rem), base + (1 if rank < rem else 0)
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def global_grid(config: str, n_gpus: int, n: int = 512):
+    pre = PRESETS[config]
+    if pre["grid"] is None:  # weak scaling: n^3 per GPU, stacked in z
+        return n, n, n * n_gpus
+    return pre["grid"]
 
+
+def layout_bytes(spec, nx, ny, nz, halo=0):
+    """Bytes of one padded grid of the library's layout (no GPU call)."""
     from stencil_amd import _lib
-    from stencil_amd.engine import JacobiEngine, StencilSpec, copy_bandwidth
-    from stencil_amd.slab import (HostStagedExchanger, LoopbackExchanger, SelfP2PExchanger, SlabInfo, SlabJacobi,
-                                  TorchDistExchanger, partition)
+    lay = _lib.make_layout(spec.problem(nx, ny, nz) if not halo else
+                           _lib.make_problem(dims=3, dtype=_lib.F64 if spec.dtype == "fp64" else _lib.F32,
+                                             shape=_lib.BOX if spec.shape == "box" else _lib.STAR, radius=1,
+                                             nx=nx, ny=ny, nz=nz, halo=halo))
+    return int(lay.bytes), int(lay.plane) * spec.elem_bytes
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return main_slab_job(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if rank_job_wanted(args, world):
-        return main_rank_job(args, world, rank, local)
-    # 1 process, 1 GPU, the structure of an interior rank: halos = own
-    # boundary planes (periodic), by device copies or by RCCL send/recv to self
-    loop = args.exchange in ("loopback", "nccl-self")
-    if loop and world != 1:
-        raise SystemExit("--exchange loopback / nccl-self are single-process rehearsals")
-    if args.share_device:
-        if args.exchange != "host":
-            raise SystemExit("--share-device needs --exchange host (RCCL refuses two ranks on one GPU)")
-        local = 0
-    torch.cuda.set_device(local)
-    if world > 1:
-        if args.exchange == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-    elif args.exchange == "nccl-self":
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29561")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=0, world_size=1)
 
-    pre = PRESETS[args.config]
-    if world < pre["min_gpus"]:
-        raise SystemExit(f"--config {args.config} needs at least {pre['min_gpus']} GPUs (grid memory)")
-    n = args.n
-    if pre["grid"] is None:  # weak scaling: n^3 per rank
-        gnx, gny, gnz = n, n, n * world
-        first, count = rank * n, n
-    else:                    # strong scaling: the global grid split in z-slabs
-        gnx, gny, gnz = pre["grid"]
-        first, count = partition(gnz, world, rank)
-    # C3 / C4 on one GPU: two grids do not fit (C3 2 x 279 GB) or leave no room
-    # (C4 2 x 138 GB); ONE resident grid plus a rolling margin of spare planes
-    # (stencil_rolling_*, bitwise the two-grid job), the margin as deep as the
-    # free HBM allows (at most 512 planes)
-    rolling = args.config in ("C3", "C4") and world == 1 and not loop
-    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
-    multi = world > 1 or loop  # the slab round structure (exchange + two streams)
-    extra = 0
+def fuse_guess(dtype: str, shape: str, nx: int, ny: int) -> int:
+    """The sweeps one launch fuses (api.hip's iterate_tk_steps /
+    iterate_box_steps defaults): the slabs' halo depth."""
+    if shape == "box":
+        return 4 if nx * ny >= 384 * 384 else 3
+    return 5 if dtype == "fp32" and nx * ny >= (1 << 20) else 4
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
 
-    if rolling:
-        from stencil_amd.engine import RollingGrid
-        free = torch.cuda.mem_get_info(local)[0]
-        plane_b = RollingGrid.bytes_needed(spec, gnx, gny, 1, 64) - RollingGrid.bytes_needed(spec, gnx, gny, 1, 63)
-        need = RollingGrid.bytes_needed(spec, gnx, gny, gnz, 8)
-        shift = int(min(512, (free - need - (2 << 30)) // plane_b + 8))
-        if shift < 16:
-            raise SystemExit(f"--config {args.config} on one GPU needs {need / 2**30:.0f} GiB + a margin; "
-                             f"{free / 2**30:.0f} GiB free")
-        grid = RollingGrid(spec, gnx, gny, gnz, shift, device=local)
-        grid.reset("reference")
-        kname = "temporalk"
-        sweeps_per_launch = grid.sweeps_per_pass
-        grid.iterate(args.warmup)
-        barrier()
-        t0 = time.perf_counter()
-        dev_ms, kernel_launches = grid.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)[1:]
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        kernel_ms_total = dev_ms
-        cells_per_launch = float(gnx) * gny * gnz  # charged per pass of K sweeps over the whole grid
-        rolling_info = {"shift_planes": shift, "launch_planes": shift - sweeps_per_launch,
-                        "launches": kernel_launches, "grid_bytes": grid.bytes}
+def slab_plan(config: str, n_gpus: int, free_bytes: int, n: int = 512, rolling: str = "auto"):
+    """What the multi-GPU job of `config` on `n_gpus` GPUs with `free_bytes`
+    of HBM free per GPU would run: the global grid, each slab's planes and
+    bytes, and whether slabs keep two grids or ONE grid plus a rolling margin
+    (when two plus SLAB_RESERVE do not fit).  SystemExit with the reason when
+    the job cannot run (too few GPUs, not even one grid per slab fits)."""
+    from stencil_amd.engine import StencilSpec
+    pre = PRESETS[config]
+    if pre.get("dims", 3) != 3:
+        raise SystemExit(f"--config {config} is 2D: one GPU only")
+    if n_gpus < pre["min_gpus"]:
+        gx, gy, gz = global_grid(config, n_gpus, n)
+        one = layout_bytes(StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"]), gx, gy, gz)[0]
+        raise SystemExit(f"--config {config} needs at least {pre['min_gpus']} GPUs: ONE {gx}x{gy}x{gz} "
+                         f"{pre['dtype']} grid is {one / 1e9:.0f} GB, more than a GPU holds; run it as "
+                         f"`python -m torch.distributed.run --nproc-per-node {pre['min_gpus']} --master-addr 127.0.0.1 "
+                         f"bench.py --gpus {pre['min_gpus']} --config {config}`")
+    gx, gy, gz = global_grid(config, n_gpus, n)
+    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"])
+    k = fuse_guess(pre["dtype"], pre["shape"], gx, gy)
+    planes = max(partition(gz, n_gpus, r)[1] for r in range(n_gpus))
+    depth = k if n_gpus > 1 else 1
+    grid_b, plane_b = layout_bytes(spec, gx, gy, planes, halo=depth if n_gpus > 1 else 0)
+    two = 2 * grid_b + SLAB_RESERVE <= free_bytes
+    if rolling == "off" and not two:
+        raise SystemExit(f"--rolling off: two {grid_b / 1e9:.0f} GB grids per slab do not fit {free_bytes / 1e9:.0f} GB")
+    use_rolling = rolling == "on" or (rolling == "auto" and not two)
+    if use_rolling:
+        margin = min(512, (free_bytes - grid_b - SLAB_RESERVE // 2 - 256) // plane_b)
+        if margin < 4 * (k + 1):
+            raise SystemExit(f"--config {config} on {n_gpus} GPUs: one {grid_b / 1e9:.0f} GB slab grid does not fit "
+                             f"{free_bytes / 1e9:.0f} GB with a rolling margin; use more GPUs")
     else:
-        # Multi-GPU slabs keep K-deep z halos (K = sweeps one fused launch does:
-        # 4 for the 7-point star, 3 or 4 for the box) so K sweeps fuse across the
-        # exchange too (one K-plane exchange per K-sweep round).
-        fuse = JacobiEngine(spec, gnx, gny, count, device=local, allocate=False).fuse_steps
-        if world > 1 or loop:
-            spec = dataclasses.replace(spec, halo=max(2, fuse))
-        flags = (_lib.HALO_LO if rank > 0 or loop else 0) | (_lib.HALO_HI if rank < world - 1 or loop else 0)
-        eng = JacobiEngine(spec, gnx, gny, count, device=local, flags=flags)
-        if loop:
-            exchanger = LoopbackExchanger() if args.exchange == "loopback" else SelfP2PExchanger(0, 1)
-            info = SlabInfo(0, 3, first, count)  # drives the multi-rank round structure
-        else:
-            exchanger = (TorchDistExchanger if args.exchange == "nccl" else HostStagedExchanger)(rank, world)
-            info = SlabInfo(rank, world, first, count)
-        SlabJacobi.use_signal = not args.no_signal
-        SlabJacobi.use_face_signal = args.face_signal
-        slab = SlabJacobi(eng, info, exchanger, overlap=not args.no_overlap)
-        slab.init("reference")
-        kernel_id = eng.plan(12)[1]
-        kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
-        if spec.shape == "box" and kname in ("temporal2", "temporalk"):
-            kname = "boxk"  # the box's fused family (kernels_boxk.hip)
-        sweeps_per_launch = eng.fuse_steps if not multi else slab.launches_per_round()
-
-        # ---------------- warmup
-        if not multi:
-            # settle the one-time per-shape choice (packed vs equal z-chunks, timed
-            # on the first launch of a shape) outside the timed region whatever W
-            # is: one fused launch a -> b, grid a unchanged
-            eng.prepare()
-            eng.iterate(args.warmup)
-        else:
-            slab.run(args.warmup)
-        barrier()
-
-        # ---------------- timed region: exactly K sweeps
-        stream = torch.cuda.current_stream()
-        t0 = time.perf_counter()
-        if not multi:
-            _, dev_ms = eng.iterate(args.steps, stream=stream, timed=True)
-            kernel_ms_total = dev_ms
-            kernel_launches = eng.plan(args.steps)[0]
-        else:
-            slab.run(args.steps)
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.exchange == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-            dist.barrier()
-        if multi and slab.signal_timeouts():
-            raise SystemExit("a face-counter wait timed out: the slab rounds did not complete")
-        if multi:
-            # Interior launch time for the roofline, from HIP events on the
-            # interior stream over a few more rounds AFTER the timed region: the
-            # events are extra queue packets (~5 us each per round on MI355X) that
-            # the timed rounds do not carry.
-            slab.start_kernel_timing()
-            extra = max(4, min(args.steps, 8)) * slab.launches_per_round()
-            slab.run(extra)
-            kernel_ms_total, kernel_launches = slab.stop_kernel_timing()
-            if world > 1:
-                dist.barrier()
-        check = None
-        if world > 1 and not args.no_check:
-            check = verify_slabs(eng, slab, spec, (gnx, gny, gnz), world, rank, args.warmup + args.steps + extra,
-                                 args.exchange == "nccl", local)
-        # the timed launch: the whole slab (single-GPU job, or face-signalled
-        # slab rounds) or the interior between the two boundary launches
-        cells_here = float(gnx) * gny * count
-        edge = slab.depth if slab.fused else max(1, slab.depth)
-        whole = not multi or slab.signalled
-        cells_per_launch = cells_here if whole else cells_here * (count - 2 * edge) / count
-        rolling_info = None
-
-    if not multi:
-        # device time per `sweeps_per_launch` sweeps, charged pro rata (with
-        # K = 4 a 1000-step job is 250 fused launches; a K that does not divide
-        # the step count adds a remainder pair / single sweep)
-        launch_ms = kernel_ms_total * sweeps_per_launch / max(1, args.steps)
-    else:
-        launch_ms = kernel_ms_total / max(1, kernel_launches)
-    if rolling:
-        del grid
-        torch.cuda.empty_cache()  # the copy-kernel calibration needs 2 GiB
-    if rank == 0:
-        if rolling:
-            parallelism = ("1 GPU, ONE resident grid + a rolling margin of %d planes (stencil_rolling_iterate: "
-                           "%d-plane launches, bitwise the two-grid job)" % (shift, shift - sweeps_per_launch))
-        elif loop:
-            parallelism = ("1 GPU rehearsing an interior rank (periodic halo, two streams, " +
-                           ("device copies)" if args.exchange == "loopback" else "RCCL send/recv to self)"))
-        elif world == 1:
-            parallelism = "1 GPU, one process, the whole grid (no decomposition)"
-        else:
-            parallelism = f"z-slab x{world}, one process per GPU (torch.distributed.run)" + (
-                ", RCCL halo P2P overlapped" if args.exchange == "nccl" else ", host-staged gloo halo (rehearsal)")
-        report(args, pre, spec, kname, (gnx, gny, gnz), world, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
-               kernel_launches, parallelism,
-               rounds=(None if not multi else "one face-signalled launch per round" if slab.signalled else
-                       "boundary + interior launches per round"),
-               launch_timing=("hipEvents of stencil_rolling_iterate over the timed region" if rolling else
-                              "hipEvents of stencil_iterate over the timed region" if not multi else
-                              "events around the face-signalled whole-slab launches of extra rounds after the timed "
-                              "region" if slab.signalled else
-                              "events around the interior launches of extra rounds after the timed region"),
-               workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu" + (f"_slab_x{world}" if multi else ""))
-               if args.config == "C2" else
-               ("C3_rolling_4096" if rolling and args.config == "C3" else f"{args.config}_rolling" if rolling else
-                f"{args.config}_slab_{count}" + (f"_x{world}" if multi else "")),
-               local=local, check=(check if world > 1 else None), cpu=(world == 1 and not loop),
-               extra_config={"rolling": rolling_info} if rolling else None,
-               kernels_per_launch=(kernel_launches / max(1.0, args.steps / sweeps_per_launch)) if rolling else 1.0)
-    if world > 1 or args.exchange == "nccl-self":
-        dist.destroy_process_group()
-
-
-def rank_job_wanted(args, world: int) -> bool:
-    """Under torch.distributed.run with N > 1: the C-ABI rank-mode job unless
-    --driver python or a rehearsal transport asks for the Python slab driver."""
-    if world <= 1 or args.driver == "python":
-        return False
-    if args.exchange != "nccl" or args.share_device or args.no_signal or args.face_signal or args.no_overlap:
-        if args.driver == "cabi":
-            raise SystemExit("--driver cabi: RCCL between distinct GPUs, default rounds (drop --exchange / "
-                             "--share-device / --no-signal / --face-signal / --no-overlap, or use --driver python)")
-        return False
-    return True
+        margin = 0
+    return {"grid": (gx, gy, gz), "planes_per_slab": planes, "grid_bytes_per_slab": grid_b, "plane_bytes": plane_b,
+            "rolling": bool(use_rolling), "margin_estimate": int(margin),
+            "scaling": "weak" if pre["grid"] is None else "strong"}
 
 
 def slab_job_plan(args, visible: int):
@@ -455,8 +280,8 @@ def slab_job_plan(args, visible: int):
     it cannot run here."""
     n = args.gpus
     if args.exchange not in ("nccl", "copy"):
-        raise SystemExit(f"--exchange {args.exchange} is a torch.distributed rehearsal: without a launcher use "
-                         "nccl (RCCL) or copy (device copies)")
+        raise SystemExit(f"--exchange {args.exchange} is an N=1 interior-rank rehearsal; with --gpus {n} use nccl "
+                         "(RCCL) or copy (device copies)")
     if args.share_device:
         if args.exchange != "copy":
             raise SystemExit("--share-device without a launcher needs --exchange copy (RCCL refuses two slabs on "
@@ -469,131 +294,322 @@ def slab_job_plan(args, visible: int):
     return list(range(n)), "rccl" if args.exchange == "nccl" else "copy"
 
 
-def global_grid_check(spec, grid, sweeps, got, device):
-    """The multi-GPU job's per-plane sums `got` against the same sweeps of the
-    global grid run as ONE grid on `device`, bit for bit (skipped when the
-    global grid does not fit beside the job)."""
+# ------------------------------------------------------------------ checks
+def reference_plane_sums(spec, grid, sweeps, device, force_reduced=False):
+    """Per-plane sums of the global grid after `sweeps` sweeps from the
+    reference initial condition, computed on ONE grid on `device`.  When the
+    global grid's two buffers do not fit, the size-independent form: the
+    reference initial condition is the same in every interior plane, so after
+    t sweeps a plane more than t planes from both z ends equals the middle
+    plane of a (2t + 1)-plane grid, and a plane within t of an end equals the
+    plane as far from that end of the small grid -- every plane's sum is
+    checked, from a grid of 2t + 1 planes.  Returns (sums, how)."""
     import numpy as np
     import torch
 
     from stencil_amd.engine import JacobiEngine
     gnx, gny, gnz = grid
+    free = torch.cuda.mem_get_info(device)[0]
+    t = int(sweeps) * spec.radius
+    full_b = 2.2 * gnx * gny * gnz * spec.elem_bytes
+    if (full_b <= 0.9 * free and not force_reduced) or gnz <= 2 * t + 1:
+        nzs = gnz
+    else:
+        nzs = 2 * t + 1
+        if 2.2 * gnx * gny * nzs * spec.elem_bytes > 0.9 * free:
+            raise RuntimeError(f"even the {nzs}-plane reference grid does not fit {free / 1e9:.0f} GB")
+    ref = JacobiEngine(spec, gnx, gny, nzs, device=device)
+    ref.reset("reference")
+    fin, _ = ref.iterate(sweeps)
+    small = ref.plane_sums(fin)
+    del ref, fin
+    torch.cuda.empty_cache()
+    if nzs == gnz:
+        return small, "the global grid as one grid, same sweeps"
+    z = np.arange(gnz)
+    idx = np.where(z < t, z, np.where(z >= gnz - t, nzs - (gnz - z), t))
+    return small[idx], (f"size-independent: every plane against a {nzs}-plane grid after the same {sweeps} sweeps "
+                        f"(the reference initial condition is z-uniform: planes > {t} from both ends equal its "
+                        "middle plane, the others its plane as far from the same end)")
+
+
+def global_grid_check(spec, grid, sweeps, got, device):
+    """The multi-GPU job's per-plane sums `got` against the same sweeps of one
+    grid on `device` (reference_plane_sums), bit for bit."""
+    import numpy as np
     try:
-        need = 2.2 * gnx * gny * gnz * spec.elem_bytes
-        free = torch.cuda.mem_get_info(device)[0]
-        if need > 0.9 * free:
-            return {"skipped": f"global grid needs {need / 1e9:.0f} GB, {free / 1e9:.0f} GB free on GPU {device}"}
-        ref = JacobiEngine(spec, gnx, gny, gnz, device=device)
-        ref.reset("reference")
-        fin, _ = ref.iterate(sweeps)
-        want = ref.plane_sums(fin)
+        want, how = reference_plane_sums(spec, grid, sweeps, device)
         bad = int(np.count_nonzero(want.view(np.uint64) != got.view(np.uint64)))
-        del ref, fin
-        torch.cuda.empty_cache()
-        return {"planes": int(gnz), "sweeps": int(sweeps), "planes_differing": bad, "bitwise_equal": bad == 0,
-                "reference": f"the global grid as one grid on GPU {device}, same sweeps, per-plane sums"}
+        return {"planes": int(grid[2]), "sweeps": int(sweeps), "planes_differing": bad, "bitwise_equal": bad == 0,
+                "reference": f"{how}, per-plane sums on GPU {device}"}
     except Exception as exc:  # a check, never the measurement
         return {"error": f"{type(exc).__name__}: {exc}"[:300]}
 
 
-def main_rank_job(args, world, rank, local):
+# ------------------------------------------------------------------- drivers
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        return main_rank_job(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
+    if args.gpus > 1 or args.exchange in ("loopback", "nccl-self"):
+        return main_slab_job(args)
+    if args.config == "C1":
+        return main_2d(args)
+    return main_single(args)
+
+
+def main_single(args):
+    """N = 1: the whole grid on one GPU -- two grids, or (C3 / C4) ONE grid plus
+    a rolling margin of spare planes (stencil_rolling_*)."""
+    import torch
+
+    from stencil_amd.engine import JacobiEngine, RollingGrid, StencilSpec
+    pre = PRESETS[args.config]
+    if pre["min_gpus"] > 1:
+        slab_plan(args.config, 1, 0, args.n)  # raises the reason
+    gnx, gny, gnz = global_grid(args.config, 1, args.n)
+    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
+    torch.cuda.set_device(0)
+    rolling = args.config in ("C3", "C4")
+    if rolling:
+        free = torch.cuda.mem_get_info(0)[0]
+        plane_b = RollingGrid.bytes_needed(spec, gnx, gny, 1, 64) - RollingGrid.bytes_needed(spec, gnx, gny, 1, 63)
+        need = RollingGrid.bytes_needed(spec, gnx, gny, gnz, 8)
+        shift = int(min(512, (free - need - (2 << 30)) // plane_b + 8))
+        if shift < 16:
+            raise SystemExit(f"--config {args.config} on one GPU needs {need / GiB:.0f} GiB + a margin; "
+                             f"{free / GiB:.0f} GiB free")
+        grid = RollingGrid(spec, gnx, gny, gnz, shift, device=0)
+        grid.reset("reference")
+        kname = "temporalk"
+        sweeps_per_launch = grid.sweeps_per_pass
+        grid.iterate(args.warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev_ms, kernel_launches = grid.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)[1:]
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kernel_ms_total = dev_ms
+        cells_per_launch = float(gnx) * gny * gnz  # charged per pass of K sweeps over the whole grid
+        extra = {"rolling": {"shift_planes": shift, "launch_planes": shift - sweeps_per_launch,
+                             "launches": kernel_launches, "grid_bytes": grid.bytes}}
+        kernels_per_launch = kernel_launches / max(1.0, args.steps / sweeps_per_launch)
+        del grid
+        torch.cuda.empty_cache()  # the copy-kernel calibration needs 2 GiB
+        parallelism = ("1 GPU, ONE resident grid + a rolling margin of %d planes (stencil_rolling_iterate: "
+                       "%d-plane launches, bitwise the two-grid job)" % (shift, shift - sweeps_per_launch))
+        timing = "hipEvents of stencil_rolling_iterate over the timed region"
+        key = "C3_rolling_4096" if args.config == "C3" else f"{args.config}_rolling"
+    else:
+        eng = JacobiEngine(spec, gnx, gny, gnz, device=0)
+        eng.reset("reference")
+        kernel_id = eng.plan(12)[1]
+        kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
+        if spec.shape == "box" and kname in ("temporal2", "temporalk"):
+            kname = "boxk"  # the box's fused family (kernels_boxk.hip)
+        sweeps_per_launch = eng.fuse_steps
+        # settle the one-time per-shape choice (packed vs equal z-chunks, timed
+        # on the first launch of a shape) outside the timed region whatever W
+        # is: one fused launch a -> b, grid a unchanged
+        eng.prepare()
+        eng.iterate(args.warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, kernel_ms_total = eng.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kernel_launches = eng.plan(args.steps)[0]
+        cells_per_launch = float(gnx) * gny * gnz
+        extra, kernels_per_launch = None, 1.0
+        parallelism = "1 GPU, one process, the whole grid (no decomposition)"
+        timing = "hipEvents of stencil_iterate over the timed region"
+        key = f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz}"
+        del eng
+    # device time per `sweeps_per_launch` sweeps, charged pro rata (with K = 4
+    # a 1000-step job is 250 fused launches; a K that does not divide the step
+    # count adds a remainder pair / single sweep)
+    launch_ms = kernel_ms_total * sweeps_per_launch / max(1, args.steps)
+    report(args, pre, spec, kname, (gnx, gny, gnz), 1, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
+           kernel_launches, parallelism, rounds=None, launch_timing=timing, workload_key=key, local=0, check=None,
+           cpu=True, extra_config=extra, kernels_per_launch=kernels_per_launch)
+
+
+def main_2d(args):
+    """BASELINE config 1, the reference's own case (run.sh: -s 1024 -i 100):
+    2D 5-point 1024^2 fp64 through AUTO (tb2ds, K sweeps per launch).  The
+    grid is 16.8 MB: launch- and barrier-latency bound, not HBM bound -- the
+    line reports us per sweep beside the Gcell/s, and the CPU baseline runs
+    the whole config on the host (1 thread and all cores)."""
+    import torch
+
+    from stencil_amd.engine import JacobiEngine, StencilSpec
+    pre = PRESETS["C1"]
+    nx, ny, _ = pre["grid"]
+    spec = StencilSpec(dims=2, dtype=pre["dtype"], shape="star", radius=1, order="naive", kernel=args.kernel)
+    torch.cuda.set_device(0)
+    eng = JacobiEngine(spec, nx, ny, 1, device=0)
+    eng.reset("reference")
+    launches, _ = eng.plan(args.steps)
+    eng.iterate(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, dev_ms = eng.iterate(args.steps, stream=torch.cuda.current_stream(), timed=True)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    sweeps_per_launch = args.steps / max(1, launches)
+    launch_ms = dev_ms / max(1, launches)
+    report(args, pre, spec, "tb2ds", (nx, ny, 1), 1, elapsed, launch_ms, float(nx) * ny, sweeps_per_launch,
+           launches, "1 GPU, one process, the whole grid", rounds=None,
+           launch_timing="hipEvents of stencil_iterate over the timed region", workload_key="C1_2d_1024",
+           local=0, check=None, cpu=True,
+           extra_config={"us_per_sweep_device": round(dev_ms * 1e3 / max(1, args.steps), 3),
+                         "bound": "launch + per-sweep barrier latency (a 16.8 MB grid; DESIGN.md §5, §9.3)"},
+           cpu_full=True)
+
+
+def _slab_spec(args, pre):
+    from stencil_amd.engine import StencilSpec
+    return StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
+
+
+def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, barrier=None):
+    """The per-rank body of the rank-mode job: build this rank's slab, warm
+    up, time exactly args.steps sweeps, time the compute launches of extra
+    rounds, collect this rank's per-plane sums.  Returns a dict (no
+    torch.distributed call: `barrier` is the caller's)."""
+    from stencil_amd.engine import SlabJob
+    gnx, gny, gnz = grid
+    job = SlabJob(spec, gnx, gny, gnz, [device], rank=(world, rank, uid), rolling=rolling, margin=0, lib=lib)
+    try:
+        info = job.info(0)
+        roll = job.rolling_info()
+        k = info["sweeps_per_round"]
+        job.fill_initial("reference")
+        sweeps = k + 1 + args.warmup
+        job.run(k + 1)  # a full and a remainder round: both launch paths' one-time costs
+        job.run(args.warmup)
+        if barrier:
+            barrier()
+        elapsed = job.run(args.steps) * 1e-3  # this rank's rounds, its device synchronised at both ends
+        sweeps += args.steps
+        extra = k * max(4, min(args.steps // max(1, k), 8))
+        job.kernel_timing(True)
+        job.run(extra)
+        kt = job.kernel_time()
+        job.kernel_timing(False)
+        sweeps += extra
+        sums = None if args.no_check else job.plane_sums()[info["first"]:info["first"] + info["planes"]].copy()
+        return {"info": info, "rolling": roll, "k": k, "elapsed": elapsed, "kt": kt, "sweeps": sweeps, "sums": sums}
+    finally:
+        job.close()
+
+
+def main_rank_job(args, world, rank, local, lib=None, check_device=None):
     """One process per GPU (torch.distributed.run) through the C-ABI rank-mode
-    slab job (stencil_slab_unique_id / stencil_slab_create_rank, csrc/slab.hip):
-    each rank builds and runs only its own z-slab, the halos over RCCL between
-    the ranks' slabs, face-signalled rounds -- the shape of an MPI-per-rank
-    launch.  torch.distributed (gloo, host side only) hands rank 0's RCCL id to
-    the others and carries the barriers, the max-over-ranks time and the
-    per-plane sums of the check; it moves no halo data."""
+    slab job (stencil_slab_unique_id / stencil_slab_create_rank,
+    csrc/slab_core.hpp): each rank builds and runs only its own z-slab, the
+    halos over RCCL between the ranks' slabs, face-signalled rounds (rolling
+    passes for slabs whose two grids do not fit) -- the shape of an
+    MPI-per-rank launch.  torch.distributed (gloo, host side only) hands rank
+    0's RCCL id to the others and carries the barriers, the max-over-ranks
+    time and the per-plane sums of the check; it moves no halo data.  `lib`:
+    the library running the slabs (the CPU tests pass the fake device; then
+    nothing here touches a GPU and the check is the caller's)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    from stencil_amd.engine import SlabJob, StencilSpec
-
+    from stencil_amd.engine import SlabJob
     pre = PRESETS[args.config]
-    if world < pre["min_gpus"]:
-        raise SystemExit(f"--config {args.config} needs at least {pre['min_gpus']} GPUs (grid memory)")
+    on_gpu = lib is None
+    if args.exchange != "nccl" or args.share_device:
+        raise SystemExit("under torch.distributed.run the halos go over RCCL between distinct GPUs "
+                         "(--exchange nccl, no --share-device); rehearse on one GPU without a launcher")
+    free = torch.cuda.mem_get_info(local)[0] if on_gpu else (1 << 40)
+    plan = slab_plan(args.config, world, free, args.n, args.rolling)
+    spec = _slab_spec(args, pre)
     dist.init_process_group("gloo")
-    n = args.n
-    gnx, gny, gnz = (n, n, n * world) if pre["grid"] is None else pre["grid"]
-    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
-    uid = [SlabJob.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    job = SlabJob(spec, gnx, gny, gnz, [local], rank=(world, rank, uid[0]))
-    info = job.info(0)
-    k = info["sweeps_per_round"]
-    job.fill_initial("reference")
-    sweeps = k + 1 + args.warmup
-    job.run(k + 1)  # a full and a remainder round: both launch paths' one-time costs
-    job.run(args.warmup)
-    dist.barrier()
-    elapsed = job.run(args.steps) * 1e-3  # this rank's rounds, its device synchronised at both ends
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    sweeps += args.steps
-    extra = k * max(4, min(args.steps // max(1, k), 8))
-    job.kernel_timing(True)
-    job.run(extra)
-    kt = job.kernel_time()
-    job.kernel_timing(False)
-    sweeps += extra
-    check = None
-    if not args.no_check:
-        sums = job.plane_sums()  # this rank's planes filled in, the rest zero
-        mine = torch.from_numpy(sums[info["first"]:info["first"] + info["planes"]].copy())
-        width = gnz // world + 1
-        buf = torch.zeros(width, dtype=torch.float64)
-        buf[:mine.numel()] = mine
-        parts = [torch.zeros_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf)
-        counts = [None] * world
-        dist.all_gather_object(counts, info["planes"])
-        job.close()
-        if rank == 0:
+    try:
+        uid = [SlabJob.unique_id(lib=lib) if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        if on_gpu:
+            torch.cuda.set_device(local)
+        res = rank_job_run(args, world, rank, local, spec, plan["grid"], plan["rolling"], uid[0], lib=lib,
+                           barrier=dist.barrier)
+        t = torch.tensor([res["elapsed"]], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        got = None
+        if not args.no_check:
+            width = plan["grid"][2] // world + 1
+            buf = torch.zeros(width, dtype=torch.float64)
+            buf[:len(res["sums"])] = torch.from_numpy(res["sums"])
+            parts = [torch.zeros_like(buf) for _ in range(world)]
+            dist.all_gather(parts, buf)
+            counts = [partition(plan["grid"][2], world, r)[1] for r in range(world)]
             got = np.concatenate([parts[r].numpy()[:counts[r]] for r in range(world)])
-            check = global_grid_check(spec, (gnx, gny, gnz), sweeps, got, local)
+        check = None
+        if rank == 0 and got is not None and on_gpu:
+            check = global_grid_check(spec, plan["grid"], res["sweeps"], got, local)
         dist.barrier()
-    else:
-        job.close()
+    finally:
+        dist.destroy_process_group()
     if rank == 0:
+        kt = res["kt"]
+        roll = res["rolling"]
         kname = "boxk" if spec.shape == "box" else "temporalk"
         parallelism = (f"z-slab x{world}, one process per GPU (torch.distributed.run) through the C-ABI rank-mode "
-                       "slab job (stencil_slab_create_rank), RCCL send/recv between the ranks' slabs")
-        report(args, pre, spec, kname, (gnx, gny, gnz), world, elapsed, kt["total_ms"] / max(1, kt["launches"]),
-               float(kt["cells_per_launch"]), k, kt["launches"], parallelism,
-               rounds="one face-signalled launch per round" if kt["signalled"] else
-               "boundary + interior launches per round",
-               launch_timing="hipEvents around rank 0's " + ("whole-slab face-signalled" if kt["signalled"] else
-                                                             "interior") + " launches of extra rounds after the timed region",
-               workload_key=f"3d7pt_fp64_{n}cube_per_gpu_slab_x{world}" if args.config == "C2" else
-               f"{args.config}_slab_{info['planes']}_x{world}",
-               local=local, check=check, cpu=False)
-    dist.destroy_process_group()
+                       "slab job (stencil_slab_create_rank), RCCL send/recv between the ranks' slabs" +
+                       (f"; ONE grid per slab + a rolling margin of {roll['margin']} planes" if roll["margin"] else ""))
+        form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
+            "boundary + interior launches"
+        line = report(args, pre, spec, kname, plan["grid"], world, elapsed, kt["total_ms"] / max(1, kt["launches"]),
+                      float(kt["cells_per_launch"]), res["k"], kt["launches"], parallelism,
+                      rounds=form, launch_timing=f"hipEvents around rank 0's {form} of extra rounds after the timed "
+                                                 "region",
+                      workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu_slab_x{world}" if args.config == "C2" else
+                                    f"{args.config}_slab_{res['info']['planes']}_x{world}"),
+                      local=local, check=check if on_gpu else {"skipped": "no GPU (CPU rehearsal)"}, cpu=False,
+                      kernels_per_launch=float(max(1, roll["launches_per_pass"])) if roll["margin"] else 1.0,
+                      extra_config={"slab_plan": {k: v for k, v in plan.items() if k != "grid"}},
+                      calibrate=on_gpu, emit=on_gpu)
+        return line, got, res
+    return None, got, res
 
 
 def main_slab_job(args):
-    """--gpus N without a launcher: ONE process drives N GPUs through the C-ABI
-    slab job (stencil_slab_create/run/plane_sums, csrc/slab.hip): z-slabs, one
-    per GPU, RCCL send/recv from one host thread, face-signalled rounds -- the
+    """Without a launcher: ONE process drives N GPUs through the C-ABI slab job
+    (stencil_slab_create/run/plane_sums, csrc/slab_core.hpp): z-slabs, one per
+    GPU, RCCL send/recv from one host thread, face-signalled rounds -- the
     shape of the reference's one spawn/join of its whole decomposed job
-    (src/stencil/stencil.cpp:34-53).  Same JSON line as the per-process
-    driver; the roofline from hipEvents on slab 0's compute stream over extra
-    rounds after the timed region; multi_gpu_check against the global grid run
-    as one grid on GPU 0."""
+    (src/stencil/stencil.cpp:34-53).  At N = 1 with --exchange loopback /
+    nccl-self: one periodic slab (its halos are its own faces) -- an interior
+    rank's rounds on one GPU.  Same JSON line as the per-process driver; the
+    roofline from hipEvents on slab 0's compute stream over extra rounds after
+    the timed region; multi_gpu_check against one grid on GPU 0."""
     import torch
 
-    from stencil_amd.engine import SlabJob, StencilSpec
-
-    devices, exchange = slab_job_plan(args, torch.cuda.device_count())
-    n_gpus = args.gpus
+    from stencil_amd.engine import SlabJob
     pre = PRESETS[args.config]
-    n = args.n
-    gnx, gny, gnz = (n, n, n * n_gpus) if pre["grid"] is None else pre["grid"]
-    spec = StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
-    job = SlabJob(spec, gnx, gny, gnz, devices, exchange=exchange)
+    loop = args.gpus == 1 and args.exchange in ("loopback", "nccl-self")
+    if loop:
+        devices, exchange = [0], ("copy" if args.exchange == "loopback" else "rccl")
+    else:
+        devices, exchange = slab_job_plan(args, torch.cuda.device_count())
+    n_gpus = args.gpus
+    free = torch.cuda.mem_get_info(0)[0]
+    shared = len(set(devices)) < len(devices)
+    # slabs sharing GPU 0 share its memory too
+    plan = slab_plan(args.config, n_gpus, free // (n_gpus if shared else 1), args.n, args.rolling)
+    spec = _slab_spec(args, pre)
+    gnx, gny, gnz = plan["grid"]
+    job = SlabJob(spec, gnx, gny, gnz, devices, exchange=exchange, periodic=loop, rolling=plan["rolling"], margin=0)
     job.fill_initial("reference")
     k = job.info(0)["sweeps_per_round"]
+    roll = job.rolling_info()
     # one full round and one shorter remainder round before the timed region:
     # the one-time costs of both launch paths (schedule trials, first launches)
     sweeps = k + 1 + args.warmup
@@ -607,27 +623,34 @@ def main_slab_job(args):
     kt = job.kernel_time()
     job.kernel_timing(False)
     sweeps += extra
-    check = None
-    if not args.no_check:
-        check = global_grid_check(spec, (gnx, gny, gnz), sweeps, job.plane_sums(), 0)
+    sums = job.plane_sums() if not (args.no_check or loop) else None
     job.close()
+    check = None if sums is None else global_grid_check(spec, plan["grid"], sweeps, sums, 0)
     kname = "boxk" if spec.shape == "box" else "temporalk"
-    where = "GPU 0 shared by every slab (rehearsal)" if args.share_device else f"{n_gpus} GPUs"
-    parallelism = (f"z-slab x{n_gpus}, ONE process driving {where} through the C-ABI slab job (stencil_slab_*), " +
-                   ("RCCL send/recv (ncclCommInitAll)" if exchange == "rccl" else "device-copy halos"))
-    report(args, pre, spec, kname, (gnx, gny, gnz), n_gpus, elapsed, kt["total_ms"] / max(1, kt["launches"]),
-           float(kt["cells_per_launch"]), k, kt["launches"], parallelism,
-           rounds="one face-signalled launch per round" if kt["signalled"] else "boundary + interior launches per round",
-           launch_timing="hipEvents around slab 0's " + ("whole-slab face-signalled" if kt["signalled"] else "interior")
-                         + " launches of extra rounds after the timed region",
-           workload_key=(f"3d7pt_fp64_{n}cube_per_gpu_slab_x{n_gpus}" if args.config == "C2" else
-                         f"{args.config}_slab_{gnz // n_gpus}_x{n_gpus}"),
-           local=0, check=check, cpu=False)
+    form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
+        "boundary + interior launches"
+    if loop:
+        parallelism = ("1 GPU rehearsing an interior rank: one periodic slab whose halos are its own faces, " +
+                       ("device copies" if exchange == "copy" else "RCCL send/recv to itself") +
+                       " (C-ABI slab job)")
+    else:
+        where = "GPU 0 shared by every slab (rehearsal)" if args.share_device else f"{n_gpus} GPUs"
+        parallelism = (f"z-slab x{n_gpus}, ONE process driving {where} through the C-ABI slab job (stencil_slab_*), " +
+                       ("RCCL send/recv (ncclCommInitAll)" if exchange == "rccl" else "device-copy halos") +
+                       (f"; ONE grid per slab + a rolling margin of {roll['margin']} planes" if roll["margin"] else ""))
+    report(args, pre, spec, kname, plan["grid"], n_gpus, elapsed, kt["total_ms"] / max(1, kt["launches"]),
+           float(kt["cells_per_launch"]), k, kt["launches"], parallelism, rounds=form,
+           launch_timing=f"hipEvents around slab 0's {form} of extra rounds after the timed region",
+           workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu_slab_x{n_gpus}" if args.config == "C2" else
+                         f"{args.config}_slab_{gnz // n_gpus}_x{n_gpus}") + ("_loop" if loop else ""),
+           local=0, check=check if n_gpus > 1 else None, cpu=False,
+           kernels_per_launch=float(max(1, roll["launches_per_pass"])) if roll["margin"] else 1.0,
+           extra_config={"slab_plan": {k2: v for k2, v in plan.items() if k2 != "grid"}})
 
 
 def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
            kernel_launches, parallelism, rounds, launch_timing, workload_key, local, check, cpu, extra_config=None,
-           kernels_per_launch=1.0):
+           kernels_per_launch=1.0, calibrate=True, emit=True, cpu_full=False):
     """Print the one JSON line.  Roofline of the dominant kernel: one launch
     advances its cells by `sweeps_per_launch` fused sweeps; its compulsory HBM
     traffic is one read plus one write of those cells (2 * sizeof(T) per cell,
@@ -637,19 +660,19 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
     `effective_GBps`.  kernels_per_launch: kernel launches per charged
     "launch" (a rolling pass runs several z-range launches; the PMC table
     holds bytes per kernel launch)."""
-    from stencil_amd.engine import copy_bandwidth
     gnx, gny, gnz = grid
     total_updates = float(gnx) * gny * gnz * args.steps
     gcell = total_updates / elapsed / 1e9
     bytes_per_update = 2 * spec.elem_bytes
     compulsory_bytes_launch = cells_per_launch * bytes_per_update
     alg_bytes_launch = compulsory_bytes_launch * sweeps_per_launch
-    achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9
-    effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9
+    achieved = compulsory_bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    effective = alg_bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     traffic, traffic_entry = load_traffic(workload_key, kname)
     if traffic:
         traffic = traffic * kernels_per_launch
     desc = pre["desc"].format(n=args.n)
+    gdesc = f"{gnx}x{gny}" + (f"x{gnz}" if pre.get("dims", 3) == 3 else "")
     out = {
         "metric": METRIC,
         "value": round(gcell, 3),
@@ -664,8 +687,8 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
         "dtype": "f64" if spec.dtype == "fp64" else "f32",
         "data": "synthetic: the reference initial condition (x-ghost faces 1, everything else 0)",
         "config": {
-            "workload": f"{desc} (global {gnx}x{gny}x{gnz}), one step = one sweep",
-            "grid": [gnx, gny, gnz],
+            "workload": f"{desc} (global {gdesc}), one step = one sweep",
+            "grid": [gnx, gny, gnz] if pre.get("dims", 3) == 3 else [gnx, gny],
             "kernel": kname,
             "parallelism": parallelism,
             "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
@@ -681,10 +704,10 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
             "bytes_basis": "compulsory: one read + one write of the launch's cells (2 x %d B per cell), "
-                           "%d fused sweeps per launch" % (spec.elem_bytes, sweeps_per_launch),
+                           "%g fused sweeps per launch" % (spec.elem_bytes, sweeps_per_launch),
             "compulsory_bytes_per_launch": compulsory_bytes_launch,
             "effective_GBps": round(effective, 1),
-            "effective_basis": "SURVEY 8(d) algorithmic: 2 x %d B per cell-update x %d sweeps per launch"
+            "effective_basis": "SURVEY 8(d) algorithmic: 2 x %d B per cell-update x %g sweeps per launch"
                                % (spec.elem_bytes, sweeps_per_launch),
             "alg_bytes_per_launch": alg_bytes_launch,
             "mean_launch_ms": round(launch_ms, 5),
@@ -696,6 +719,9 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
         out["config"].update(extra_config)
     if n_gpus > 1:
         out["multi_gpu_check"] = check if check is not None else {"skipped": "--no-check"}
+        out["multi_gpu_status"] = ("the rounds' code (csrc/slab_core.hpp) is bitwise-tested at world 2/3 on the CPU "
+                                   "(tests/test_slab_core_cpu.py) and as slabs sharing one GPU; this line's "
+                                   "multi_gpu_check is its check on distinct GPUs")
     if traffic_entry is not None:
         out["roofline"]["traffic_source"] = {k: traffic_entry.get(k) for k in
                                              ("source", "kernel", "kernel_source_sha", "fresh")}
@@ -705,19 +731,29 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
         # above the compulsory bytes = re-reads (tile rings, halos)
         out["roofline"]["traffic_GBps"] = round(traffic / (launch_ms * 1e-3) / 1e9, 1)
         out["roofline"]["traffic_frac"] = round(out["roofline"]["traffic_GBps"] / HBM_PEAK_GBPS, 4)
-    try:
-        out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
-    except Exception as exc:  # calibration only
-        out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
+    if calibrate:
+        try:
+            from stencil_amd.engine import copy_bandwidth
+            out["roofline"]["copy_kernel_GBps"] = round(copy_bandwidth(1 << 30, reps=10, device=local), 1)
+        except Exception as exc:  # calibration only
+            out["roofline"]["copy_kernel_GBps"] = f"unavailable: {exc}"
     if cpu and not args.no_cpu_baseline:
         cb = dict(dtype=spec.dtype, shape=spec.shape)
-        n = min(args.n, 512)
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds, **cb)
-        # the same loop with OpenMP over the host's cores too
-        out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads(), **cb)
+        if cpu_full:  # the whole 2D config on the host (C1: 1024^2 x steps)
+            n = gnx
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds, dims=2, iters_cap=args.steps, **cb)
+            out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads(), dims=2,
+                                                         iters_cap=args.steps, **cb)
+        else:
+            n = min(args.n, 512)
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds, **cb)
+            # the same loop with OpenMP over the host's cores too
+            out["cpu_baseline_all_cores"] = cpu_baseline(n, args.cpu_seconds / 2, threads=host_threads(), **cb)
     else:
         out["cpu_baseline"] = None
-    print(json.dumps(out), flush=True)
+    if emit:
+        print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

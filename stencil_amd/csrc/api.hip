@@ -449,7 +449,7 @@ int stencil_sweep(const stencil_layout* l, const void* in, void* out, int64_t be
     // A 3D slab may also advance the halo planes of a face shared with a
     // neighbour (HALO_LO/HI) as deep as its ghost layers allow beyond the
     // stencil radius: two sweeps per 2-plane exchange (communication-avoiding
-    // temporal blocking, stencil_amd/slab.py).
+    // temporal blocking across slabs).
     const int64_t ext = l->prob.dims == 3 ? l->zghost - l->prob.radius : 0;
     const int64_t lo = (l->prob.flags & STENCIL_HALO_LO) ? -ext : 0;
     const int64_t hi = stencil_slow_extent(l) + ((l->prob.flags & STENCIL_HALO_HI) ? ext : 0);

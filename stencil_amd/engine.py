@@ -3,7 +3,7 @@ HIP kernel launched through the C-ABI (stencil_amd/_lib.py).
 
 This is the Python counterpart of the C++ host engine (csrc/host/stencil.cpp,
 itself the mirror of the reference's class Stencil, src/stencil/stencil.cpp).
-It exposes what the benchmark, the tests and the multi-GPU slab driver need:
+It exposes what the benchmark and the tests need:
 two ping-pong grids in the engine's padded layout, the reference initial
 condition, single sweeps over slow-axis ranges, the whole-job iterate, and
 views of whole planes for halo exchange.
@@ -341,10 +341,11 @@ def copy_bandwidth(nbytes: int, reps: int = 20, device: int = 0) -> float:
 
 
 class SlabJob:
-    """A multi-GPU z-slab job run by the C++ host (stencil_slab_*, csrc/slab.hip):
-    one process, `devices` one slab each, halos over RCCL (or device copies,
-    which let several slabs share a GPU).  The counterpart of slab.py's
-    per-process driver for callers without torch.distributed."""
+    """A multi-GPU z-slab job run by the C++ host (stencil_slab_*: the rounds
+    in csrc/slab_core.hpp, bound to HIP + RCCL in csrc/slab.hip): one process
+    and `devices` one slab each, halos over RCCL (or device copies, which let
+    several slabs share a GPU), or -- rank mode -- this process's one slab of
+    a job whose other slabs live in other processes."""
 
     def __init__(self, spec: StencilSpec, nx: int, ny: int, nz: int, devices, exchange: str = "rccl",
                  periodic: bool = False, rank=None, rolling: bool = False, margin: int = 0, lib=None):

@@ -15,17 +15,26 @@
 //              the cut ends stand still like ghost planes, which reaches K r
 //              planes inward after K sweeps and so never [begin, end)
 //   face-signalled launches: the sweep plus one add per face to the counters
-//   communicator: an in-process mailbox, one FIFO per (communicator id,
-//              sender, receiver) -- sends are buffered copies, receives match
-//              in posting order as NCCL's do, a group's receives complete at
-//              its end (blocking, with a timeout instead of a hang); rank-mode
-//              jobs in several threads of one process join by their id
+//   communicator: a mailbox, one FIFO per (communicator id, sender,
+//              receiver) -- sends are buffered copies, receives match in
+//              posting order as NCCL's do, a group's receives complete at its
+//              end (blocking, with a timeout instead of a hang).  In memory for
+//              the ranks of one process (rank-mode jobs in threads join by
+//              their id); with FAKE_SLAB_MAILBOX_DIR set, files in that
+//              directory (one per message, written then renamed), so ranks in
+//              separate processes -- bench.py's gloo-launched ranks in the CPU
+//              tests -- exchange their halos too
 //
 // Exported with the fake_slab_ prefix and the stencil_slab_* signatures
 // (tests/cpu_slab/binding.py maps them onto stencil_amd.engine.SlabJob).
 // Never linked into the product: it links liboracle.so.
+#include <unistd.h>
+
 #include <chrono>
 #include <condition_variable>
+#include <fstream>
+#include <sstream>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -98,7 +107,66 @@ struct PendingRecv {
 thread_local int t_group = 0;
 thread_local std::vector<PendingRecv> t_pending;
 
+// ---- the cross-process form: FAKE_SLAB_MAILBOX_DIR
+const char* mail_dir() {
+    const char* d = std::getenv("FAKE_SLAB_MAILBOX_DIR");
+    return d && *d ? d : nullptr;
+}
+std::string hex_of(const std::string& id) {
+    static const char* k = "0123456789abcdef";
+    std::string h;
+    for (unsigned char ch : id) {
+        if (!ch) break;
+        h += k[ch >> 4];
+        h += k[ch & 15];
+    }
+    return h.substr(0, 48);
+}
+// per (id, from, to) message counters of THIS process (sends / receives)
+std::mutex g_seq_mu;
+std::map<std::tuple<std::string, int, int>, int64_t> g_sent, g_taken;
+std::string mail_path(const std::string& id, int from, int to, int64_t seq) {
+    std::ostringstream o;
+    o << mail_dir() << "/m_" << hex_of(id) << "_" << from << "_" << to << "_" << seq;
+    return o.str();
+}
+int file_send(const void* p, size_t bytes, int from, int to, const std::string& id) {
+    int64_t seq;
+    {
+        std::lock_guard<std::mutex> lk(g_seq_mu);
+        seq = g_sent[std::make_tuple(id, from, to)]++;
+    }
+    const std::string path = mail_path(id, from, to, seq), tmp = path + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        f.write(static_cast<const char*>(p), std::streamsize(bytes));
+        if (!f) return set_error(STENCIL_EHIP, "fake send: cannot write %s", tmp.c_str());
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) return set_error(STENCIL_EHIP, "fake send: rename failed");
+    return STENCIL_OK;
+}
+int file_take(void* p, size_t bytes, int from, int to, const std::string& id) {
+    int64_t seq;
+    {
+        std::lock_guard<std::mutex> lk(g_seq_mu);
+        seq = g_taken[std::make_tuple(id, from, to)]++;
+    }
+    const std::string path = mail_path(id, from, to, seq);
+    for (int it = 0; access(path.c_str(), F_OK) != 0; ++it) {
+        if (it > 30000) return set_error(STENCIL_EHIP, "fake recv: rank %d waited 30 s for rank %d", to, from);
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (size_t(f.tellg()) != bytes) return set_error(STENCIL_EHIP, "fake recv: %zu bytes posted, message differs", bytes);
+    f.seekg(0);
+    f.read(static_cast<char*>(p), std::streamsize(bytes));
+    f.close();
+    std::remove(path.c_str());
+    return STENCIL_OK;
+}
+
 int take(void* p, size_t bytes, int peer, Comm* c) {
+    if (mail_dir()) return file_take(p, bytes, peer, c->rank, c->id);
     Mailbox& m = mailbox();
     std::unique_lock<std::mutex> lk(m.mu);
     const auto key = std::make_tuple(c->id, peer, c->rank);
@@ -345,6 +413,17 @@ struct FakeDev {
     }
     static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank) {
         const std::string key(static_cast<const char*>(id), STENCIL_SLAB_ID_BYTES);
+        if (fake::mail_dir()) {  // ranks in separate processes: a join file each, wait for all
+            const std::string base = std::string(fake::mail_dir()) + "/join_" + fake::hex_of(key) + "_";
+            std::ofstream(base + std::to_string(rank)) << rank;
+            for (int r = 0; r < nranks; ++r)
+                for (int it = 0; access((base + std::to_string(r)).c_str(), F_OK) != 0; ++it) {
+                    if (it > 30000) return set_error(STENCIL_EHIP, "fake comm init: rank %d never joined", r);
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                }
+            *comm = new fake::Comm{key, rank, nranks};
+            return STENCIL_OK;
+        }
         fake::Mailbox& m = fake::mailbox();
         std::unique_lock<std::mutex> lk(m.mu);
         ++m.joined[key];
@@ -371,6 +450,11 @@ struct FakeDev {
     }
     static int send(const void* p, size_t bytes, int peer, Comm c, Stream) {
         if (peer < 0 || peer >= c->nranks) return set_error(STENCIL_EINVAL, "fake send to rank %d of %d", peer, c->nranks);
+        if (fake::mail_dir()) {
+            std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+            ++fake::g_sends;
+            return fake::file_send(p, bytes, c->rank, peer, c->id);
+        }
         fake::Mailbox& m = fake::mailbox();
         {
             std::lock_guard<std::mutex> lk(m.mu);

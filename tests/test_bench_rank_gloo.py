@@ -1,0 +1,85 @@
+"""bench.py's N > 1 path on the CPU: world 2 and 3 over gloo.
+
+Under torch.distributed.run every rank runs bench.main_rank_job: rank 0's
+RCCL id broadcast over a gloo group, each rank's own C-ABI slab
+(stencil_slab_create_rank), warm-up, the timed rounds, the max-over-ranks
+time, the kernel-timing rounds and the per-plane sums gathered on rank 0.
+Here each rank is a separate process (torch.multiprocessing, gloo on
+127.0.0.1) and its slab runs on the CPU fake device of tests/cpu_slab -- the
+same csrc/slab_core.hpp rounds, oracle sweeps, halos through a file mailbox
+(FAKE_SLAB_MAILBOX_DIR).  The gathered per-plane sums must equal, bit for
+bit, those of the same job run as ONE slab.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import bench
+from stencil_amd.engine import SlabJob, StencilSpec
+from tests.cpu_slab import binding as fb
+
+pytestmark = pytest.mark.skipif(not fb.available(), reason="tests/cpu_slab/libslab_fake.so not built (run make)")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, mail, argv, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", FAKE_SLAB_MAILBOX_DIR=mail)
+    fake = fb.load()
+    fake.set_k(0)
+    args = bench.parse(argv)
+    line, got, res = bench.main_rank_job(args, world, rank, 0, lib=fake)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "got.npy"), got)
+        np.save(os.path.join(out_dir, "meta.npy"), np.array([res["sweeps"], line["value"] > 0,
+                                                             line["n_gpus"], res["k"]], dtype=np.float64))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("config,extra", [("C2", ["--n", "20"]), ("C2", ["--n", "20", "--no-signal"]),
+                                          ("C2", ["--n", "20", "--rolling", "on"])])
+def test_bench_rank_job_world_gloo(world, config, extra):
+    argv = ["--gpus", str(world), "--config", config, "--steps", "9", "--warmup", "2"] + extra
+    with tempfile.TemporaryDirectory() as tmp:
+        mail = os.path.join(tmp, "mail")
+        os.makedirs(mail)
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_rank_main, args=(r, world, port, mail, argv, tmp)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(240)
+        codes = [p.exitcode for p in procs]
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        assert codes == [0] * world, codes
+        got = np.load(os.path.join(tmp, "got.npy"))
+        sweeps, ok, n_gpus, k = np.load(os.path.join(tmp, "meta.npy"))
+        assert ok and int(n_gpus) == world
+        leftovers = os.listdir(mail)
+        assert all(f.startswith("join_") for f in leftovers), leftovers  # every halo message was received
+    # the same sweeps on ONE slab (no exchange), the fake device's plane sums
+    fake = fb.load()
+    fake.set_k(0)
+    n = 20
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, n, n, n * world, [0], exchange="rccl", lib=fake)
+    job.fill_initial("reference")
+    job.run(int(sweeps))
+    want = job.plane_sums()
+    job.close()
+    assert int(k) == 4
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))

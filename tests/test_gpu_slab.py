@@ -1,17 +1,20 @@
 """Slab decomposition with the HIP kernels, N logical slabs on one GPU.
 
-RCCL cannot put two ranks on one device, so the exchange here is a plain
-device copy between the slabs' grids (the torch.distributed exchange logic
-itself is covered by tests/test_slab_gloo.py).  What this pins is the GPU
-side of multi-GPU: 2-deep halos, the HALO_LO/HI flags of the fused kernel,
-boundary/interior plane ranges -- bitwise equal to one undivided grid."""
+RCCL cannot put two ranks on one device, so the exchange in the first tests
+is a plain device copy between the slabs' grids, written out here.  What
+they pin is the GPU side of multi-GPU: deep halos, the HALO_LO/HI flags of
+the fused kernels, boundary/interior plane ranges, the face-signalled
+launches -- bitwise equal to one undivided grid.  The round logic itself is
+the C-ABI slab job's (csrc/slab_core.hpp): its periodic one-slab rings here,
+tests/test_gpu_slab_job.py on the GPU, tests/test_slab_core_cpu.py on the
+CPU at world 2 / 3."""
 import numpy as np
 import pytest
 import torch
 
 from stencil_amd import _lib
-from stencil_amd.engine import JacobiEngine, StencilSpec
-from stencil_amd.slab import partition
+from bench import partition
+from stencil_amd.engine import JacobiEngine, SlabJob, StencilSpec
 
 pytestmark = pytest.mark.gpu
 
@@ -137,41 +140,6 @@ def test_fused_needs_deep_halo(gpu):
         e.sweep2(e.a, e.b, 0, 8)
 
 
-def _periodic_run(gpu, exchanger, nx, ny, nz, it, shape="star"):
-    """SlabJacobi on one rank whose halos are its own boundary planes."""
-    from stencil_amd.slab import SlabInfo, SlabJacobi
-    spec = StencilSpec(dims=3, dtype="fp64", shape=shape)
-    fuse = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
-    spec = StencilSpec(dims=3, dtype="fp64", shape=shape, halo=max(2, fuse))
-    e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
-    slab = SlabJacobi(e, SlabInfo(0, 3, 0, nz), exchanger)
-    slab.init("random", 5, plane_elems=nx * ny)
-    slab.run(it)
-    torch.cuda.synchronize()
-    return e.interior(slab.cur).clone()
-
-
-@pytest.mark.parametrize("shape", ["star", "box"])
-def test_rccl_self_p2p_matches_device_copies(gpu, shape):
-    """The RCCL send/recv path of the slab exchange (TorchDistExchanger's
-    batch_isend_irecv on the boundary stream, waited for on that stream), run
-    with this process as its own peer (world size 1), gives bit for bit the
-    result of the same periodic halos moved by device copies."""
-    import os
-    import torch.distributed as dist
-    from stencil_amd.slab import LoopbackExchanger, SelfP2PExchanger
-    nx, ny, nz, it = 70, 45, 33, 13
-    want = _periodic_run(gpu, LoopbackExchanger(), nx, ny, nz, it, shape)
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = "29571" if shape == "star" else "29572"
-    dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), rank=0, world_size=1)
-    try:
-        got = _periodic_run(gpu, SelfP2PExchanger(0, 1), nx, ny, nz, it, shape)
-    finally:
-        dist.destroy_process_group()
-    assert torch.equal(got, want)
-
-
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
 @pytest.mark.parametrize("steps", [3, 4, 5])
 @pytest.mark.parametrize("zchunk", ["0", "5", "9", "40"])
@@ -291,42 +259,35 @@ def test_face_signal_counts_completed_faces(gpu, dtype, steps):
     fs.close()
 
 
-def _periodic_run_sig(gpu, exchanger, nx, ny, nz, it, signalled, face_signal=True, dtype="fp64", shape="star"):
-    from stencil_amd.slab import SlabInfo, SlabJacobi
+def _periodic_job(gpu, monkeypatch, nx, ny, nz, it, signalled, dtype="fp64", shape="star", exchange="copy"):
+    """A one-slab periodic C-ABI job (its halos are its own faces: an
+    interior rank's rounds), face-signalled or boundary + interior rounds
+    (STENCIL_SLAB_SIGNAL), halos by device copies or RCCL to itself."""
+    monkeypatch.setenv("STENCIL_SLAB_SIGNAL", "1" if signalled else "0")
     spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
-    fuse = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
-    spec = StencilSpec(dims=3, dtype=dtype, shape=shape, halo=max(2, fuse))
-    e = JacobiEngine(spec, nx, ny, nz, device=gpu, flags=_lib.HALO_LO | _lib.HALO_HI)
-    SlabJacobi.use_signal = signalled
-    default_fs = SlabJacobi.use_face_signal
-    SlabJacobi.use_face_signal = face_signal
+    job = SlabJob(spec, nx, ny, nz, [gpu], exchange=exchange, periodic=True)
     try:
-        slab = SlabJacobi(e, SlabInfo(0, 3, 0, nz), exchanger)
+        job.fill_initial("random", 5)
+        job.run(it)
+        dense = job.download()
+        k = job.info(0)["sweeps_per_round"]
+        job.kernel_timing(True)
+        job.run(k)
+        assert job.kernel_time()["signalled"] == signalled
     finally:
-        SlabJacobi.use_signal = True
-        SlabJacobi.use_face_signal = default_fs
-    assert slab.signalled == signalled
-    assert (slab._fsig is not None) == (signalled and face_signal)
-    assert slab.k == fuse
-    slab.init("random", 5, plane_elems=nx * ny)
-    slab.run(it)
-    assert slab.signal_timeouts() == 0
-    torch.cuda.synchronize()
-    return e.interior(slab.cur).clone()
+        job.close()
+    return dense
 
 
-@pytest.mark.parametrize("face_signal", [True, False])
 @pytest.mark.parametrize("shape3,it", [((70, 45, 33), 13), ((130, 64, 20), 9), ((64, 7, 9), 8)])
-def test_signalled_rounds_match_boundary_launches(gpu, shape3, it, face_signal):
-    """Single-launch face-signalled slab rounds (device copies as the halo
-    transport; the exchange gated by the command processor on the face
-    signal, or by a wait kernel on the counters) give bit for bit the
-    two-boundary-launch rounds."""
-    from stencil_amd.slab import LoopbackExchanger
+def test_signalled_rounds_match_boundary_launches(gpu, monkeypatch, shape3, it):
+    """Single-launch face-signalled slab rounds (the exchange gated by the
+    wait kernel on the face counters) give bit for bit the two-boundary-launch
+    rounds."""
     nx, ny, nz = shape3
-    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False)
-    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, face_signal)
-    assert torch.equal(got, want)
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
@@ -337,61 +298,72 @@ def test_signalled_rounds_every_k(gpu, monkeypatch, dtype, steps, extra, it):
     the minimum 2K planes (the launch's chunks shrink to >= K planes each) to
     several chunks, with a remainder of iterations after the K-rounds --
     bitwise the boundary + interior rounds."""
-    from stencil_amd.slab import LoopbackExchanger
     monkeypatch.setenv("STENCIL_TK_STEPS", steps)
     nz = 2 * int(steps) + extra  # 2K planes: the smallest signalled slab
     nx, ny = 67, 29
-    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype)
-    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, False, dtype=dtype)
-    ib = torch.int64 if dtype == "fp64" else torch.int32
-    assert torch.equal(got.view(ib), want.view(ib)), (nz, it)
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, dtype=dtype)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (nz, it)
 
 
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-def test_signalled_rounds_then_remainder_large_plane(gpu, dtype):
+def test_signalled_rounds_then_remainder_large_plane(gpu, monkeypatch, dtype):
     """The round-1 stream race, made deterministic: a minimum slab (nz = 2K)
     with a 2048^2 plane, so the last face-signalled launch runs for
-    milliseconds, then a remainder pair.  The pair runs on the caller's
-    stream (n <= 2*edge), which must first join the round streams -- it
-    reads the grid the last signalled launch writes and the halos the
+    milliseconds, then a remainder round that must follow the round streams
+    -- it reads the grid the last signalled launch writes and the halos the
     exchange receives.  Bitwise the boundary + interior rounds."""
-    from stencil_amd.slab import LoopbackExchanger
     nx = ny = 2048
     fuse = JacobiEngine(StencilSpec(dims=3, dtype=dtype), nx, ny, 8, device=gpu, allocate=False).fuse_steps
     nz, it = 2 * fuse, 2 * fuse + 2  # two signalled rounds + a remainder pair
-    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype)
-    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, False, dtype=dtype)
-    ib = torch.int64 if dtype == "fp64" else torch.int32
-    assert torch.equal(got.view(ib), want.view(ib))
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, dtype=dtype)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
-@pytest.mark.parametrize("shape3,it", [((70, 45, 33), 13), ((130, 64, 20), 9), ((64, 7, 6), 8), ((64, 7, 9), 10)])
-@pytest.mark.parametrize("face_signal", [True, False])
-def test_box_signalled_rounds_match_boundary_launches(gpu, dtype, shape3, it, face_signal):
-    """27-point box slab rounds as one face-signalled launch (K = 3, the box's
-    fuse depth) give bit for bit the boundary + interior rounds, with
-    remainders after the K-rounds and the minimum slab (nz = 2K)."""
-    from stencil_amd.slab import LoopbackExchanger
+@pytest.mark.parametrize("shape3,it", [((70, 45, 33), 13), ((130, 64, 20), 9), ((64, 7, 8), 8), ((64, 7, 9), 10)])
+def test_box_signalled_rounds_match_boundary_launches(gpu, monkeypatch, dtype, shape3, it):
+    """27-point box slab rounds as one face-signalled launch give bit for bit
+    the boundary + interior rounds, with remainders after the K-rounds and the
+    minimum slab (nz = 2K)."""
     nx, ny, nz = shape3
-    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False, dtype=dtype, shape="box")
-    got = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, True, face_signal, dtype=dtype, shape="box")
-    ib = torch.int64 if dtype == "fp64" else torch.int32
-    assert torch.equal(got.view(ib), want.view(ib))
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape="box")
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, dtype=dtype, shape="box")
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
-def test_signalled_rounds_over_rccl(gpu):
-    """The same through RCCL send/recv to self (world size 1)."""
-    import os
-    import torch.distributed as dist
-    from stencil_amd.slab import LoopbackExchanger, SelfP2PExchanger
+@pytest.mark.parametrize("shape", ["star", "box"])
+def test_signalled_rounds_over_rccl(gpu, monkeypatch, shape):
+    """The same through RCCL send/recv to self (a one-device communicator)."""
     nx, ny, nz, it = 70, 45, 33, 13
-    want = _periodic_run_sig(gpu, LoopbackExchanger(), nx, ny, nz, it, False)
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = "29573"
-    dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), rank=0, world_size=1)
-    try:
-        got = _periodic_run_sig(gpu, SelfP2PExchanger(0, 1), nx, ny, nz, it, True)
-    finally:
-        dist.destroy_process_group()
-    assert torch.equal(got, want)
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, shape=shape)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, shape=shape, exchange="rccl")
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype,shape", [("fp64", "star"), ("fp32", "box")])
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+def test_rolling_slabs_equal_one_grid(gpu, dtype, shape, nslabs):
+    """ROLLING slab jobs (one grid per slab + a margin, STENCIL_SLAB_ROLLING)
+    on slabs sharing the GPU, from one-plane launches to one launch per pass:
+    bitwise one grid, and bitwise the two-grid slab job."""
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz = 70, 45, 23 * nslabs + 1
+    it = 11
+    ref = JacobiEngine(StencilSpec(dims=3, dtype=dtype, shape=shape, kernel="direct"), nx, ny, nz, device=gpu)
+    ref.reset("random", 3)
+    fin, _ = ref.iterate(it)
+    want = ref.to_numpy(fin)
+    k = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
+    for margin in (k + 1, k + 4, 64):
+        job = SlabJob(spec, nx, ny, nz, [gpu] * nslabs, exchange="copy", rolling=True, margin=margin)
+        try:
+            assert job.rolling_info()["margin"] == margin
+            job.fill_initial("random", 3)
+            job.run(k)
+            job.run(it - k)
+            got = job.download()
+        finally:
+            job.close()
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), margin

@@ -254,3 +254,52 @@ def test_bench_rank_mode_two_processes(gpu):
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["multi_gpu_check"]["bitwise_equal"], line
     assert "rank-mode" in line["config"]["parallelism"]
+
+
+def _bench_line(argv, timeout=300):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + argv, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_bench_rolling_slab_job_rehearsal(gpu):
+    """bench.py --gpus 2 --rolling on, both slabs on GPU 0 (the NS4096 N = 2
+    form at a scaled shape: ONE grid per slab plus a rolling margin, a pass of
+    z-range launches then the exchange): bitwise the global grid."""
+    line = _bench_line(["--gpus", "2", "--share-device", "--exchange", "copy", "--rolling", "on", "--n", "128",
+                        "--steps", "16", "--warmup", "4"])
+    assert line["multi_gpu_check"]["bitwise_equal"], line["multi_gpu_check"]
+    assert line["config"]["rounds"] == "rolling passes"
+    assert "rolling margin" in line["config"]["parallelism"] and line["config"]["slab_plan"]["rolling"]
+
+
+@pytest.mark.parametrize("exchange", ["loopback", "nccl-self"])
+def test_bench_interior_rank_rehearsal(gpu, exchange):
+    """--exchange loopback / nccl-self: one periodic slab through the C-ABI
+    (halos = its own faces by device copies / RCCL to itself), face-signalled
+    rounds."""
+    line = _bench_line(["--exchange", exchange, "--n", "128", "--steps", "16", "--warmup", "4"])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["config"]["rounds"] == "face-signalled launches"
+    assert "periodic slab" in line["config"]["parallelism"]
+
+
+@pytest.mark.parametrize("sweeps", [1, 6, 13])
+def test_size_independent_plane_check(gpu, sweeps):
+    """The multi-GPU check for global grids too large for one GPU (NS4096):
+    every plane's sum from a (2t + 1)-plane grid equals the full grid's,
+    bit for bit (the reference initial condition is z-uniform)."""
+    import bench
+    spec = StencilSpec(dims=3, dtype="fp64")
+    grid = (96, 80, 70)
+    full, how_full = bench.reference_plane_sums(spec, grid, sweeps, gpu)
+    red, how_red = bench.reference_plane_sums(spec, grid, sweeps, gpu, force_reduced=True)
+    assert how_full.startswith("the global grid") and how_red.startswith("size-independent")
+    assert np.array_equal(full.view(np.uint64), red.view(np.uint64))

@@ -1,0 +1,47 @@
+#!/bin/bash
+# One parameterised GPU-box script (replaces round 3's 45 per-call scripts):
+#   gpurun --timeout 1200 -- bash tools/gpu/lease.sh <tag> <step>...
+# Steps run in order, each under its own time limit, output to gpurun_out/<tag>/;
+# the first failing step ends the call (no GPU step after a failure or a timeout).
+#   tests            the whole -m gpu suite
+#   tests:<files>    -m gpu on the comma-separated test files
+#   smoke            __graft_entry__.smoke()
+#   bench            the driver's command (bench.py --gpus 1 --steps 20 --warmup 5)
+#   bench:<cfg>      bench.py --config <cfg> (C1..C5, NS) at its usual length
+#   bench1000        the default 1000-step C2 bench
+#   prof:<cfg>       profiles/collect.sh (kernel trace + FETCH/WRITE passes) of bench --config <cfg>
+#   tier             tools/tier_pattern_bench 16 and 32 (the C2 decision gate)
+#   ramp             tools/ramp_probe.py under a rocprofv3 kernel trace (per-launch durations by phase)
+set -o pipefail
+TAG=$1; shift
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R" || exit 1
+for step in "$@"; do
+  echo "[lease] $TAG: $step $(date +%T)"
+  case "$step" in
+    tests) timeout -k 10 1100 python3 -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests \
+             > "$O/gpu_tests.txt" 2>&1 ;;
+    tests:*) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+             $(echo "${step#tests:}" | tr ',' ' ') > "$O/gpu_tests_part.txt" 2>&1 ;;
+    smoke) timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench.err" ;;
+    bench1000) timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline \
+             > "$O/bench_1000.json" 2>> "$O/bench.err" ;;
+    bench:*) c=${step#bench:}
+             case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+             timeout -k 10 400 python3 bench.py --config "$c" $a > "$O/bench_$c.json" 2>> "$O/bench.err" ;;
+    prof:*) c=${step#prof:}
+            case "$c" in C5) a="--steps 8 --warmup 0";; *) a="--steps 100 --warmup 5";; esac
+            bash profiles/collect.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/collect_$c.log" 2>&1 ;;
+    tier) timeout -k 10 120 tools/tier_pattern_bench 16 > "$O/tier16.txt" 2>&1 &&
+          timeout -k 10 120 tools/tier_pattern_bench 32 > "$O/tier32.txt" 2>&1 ;;
+    ramp) (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O/ramp" -o run -- \
+             python3 "$R/tools/ramp_probe.py" > "$O/ramp.log" 2>&1) ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  if [ $rc -ne 0 ]; then echo "[lease] $TAG: step $step failed rc=$rc"; exit $rc; fi
+done
+echo "[lease] $TAG: done $(date +%T)"
