@@ -25,7 +25,10 @@ ITERATIONS = [1, 10, 100, 1000, 5000, 10000, 50000, 100000]              # run_e
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--methods", nargs="+", default=["DMA", "DMAStaticUnroll", "DMASlavePack", "RMA", "HIP"])
+    ap.add_argument("--methods", nargs="+", default=["DMA", "DMAStaticUnroll", "DMASlavePack", "RMA", "HIP", "CPU"])
+    ap.add_argument("--cpu-max-iterations", type=int, default=1000,
+                    help="run the CPU method (the reference's naive loop on the host, single-threaded) only up to "
+                         "this many iterations: at 100000 iterations of a 960^2 grid it alone takes minutes")
     ap.add_argument("--block-sizes", nargs="+", type=int, default=BLOCK_SIZES)
     ap.add_argument("--iterations", nargs="+", type=int, default=ITERATIONS)
     ap.add_argument("--repeat", type=int, default=1)
@@ -37,8 +40,9 @@ def main():
     for block_size in args.block_sizes:
         for iteration in args.iterations:
             matrix_size = block_size * 8
+            methods = [m for m in args.methods if m != "CPU" or iteration <= args.cpu_max_iterations]
             command = [args.binary, "-s", str(matrix_size), "-b", str(block_size), "-i", str(iteration),
-                       "-R", str(args.repeat), "-m", *args.methods]
+                       "-R", str(args.repeat), "-m", *methods]
             print(f'----------- block size: {block_size}, iteration: {iteration} -----------')
             result = subprocess.run(command, capture_output=True, text=True)
             output = result.stdout.strip()
@@ -52,7 +56,10 @@ def main():
             outputs.append(row)
 
     with open(args.out, 'w', newline='') as f:
-        writer = csv.DictWriter(f, fieldnames=list(outputs[0].keys()))
+        # columns of every row, first-seen order (a method dropped from some
+        # rows -- CPU past --cpu-max-iterations -- leaves those cells empty)
+        fields = list(dict.fromkeys(k for row in outputs for k in row))
+        writer = csv.DictWriter(f, fieldnames=fields)
         writer.writeheader()
         writer.writerows(outputs)
 

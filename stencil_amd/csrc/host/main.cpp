@@ -75,7 +75,8 @@ void run_test(std::string_view method_name, ProgramOptions const& options) {
     if (dev_ms > 0.0) {
         const double gcell = cells * options.iterations / (dev_ms * 1e-3) / 1e9;
         const double bytes_per_update = 2.0 * (options.fp64 ? 8.0 : 4.0);
-        std::cout << "[stencil-amd] " << method_name << ": device " << dev_ms << " ms, " << gcell
+        std::cout << "[stencil-amd] " << method_name << (method_name == "CPU" ? ": host " : ": device ") << dev_ms
+                  << " ms, " << gcell
                   << " Gcell-updates/s, " << gcell * bytes_per_update << " GB/s algorithmic\n";
     }
 }

@@ -131,6 +131,7 @@ auto Stencil::run_slabs(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std
 template <class T>
 auto Stencil::run_typed(InputMethod method, BoundaryGrid<T>& matrix, BoundaryGrid<T>& result)
     -> std::chrono::steady_clock::duration {
+    if (method == CPU) return run_cpu(matrix, result);
     initialize_matrix();
     const bool ref_variant = method == DMA || method == DMA_STATIC_UNROLL || method == DMA_SLAVE_PACK || method == RMA;
     if (method == HIP_MULTI_GPU || (options.gpus > 1 && !ref_variant)) return run_slabs(matrix, result);
@@ -250,21 +251,23 @@ auto Stencil::run(std::string_view method_name) -> std::optional<std::chrono::st
         {"HIPTemporalK", HIP_TEMPORALK},
         {"HIPPersistent", HIP_PERSISTENT},
         {"HIPMultiGPU", HIP_MULTI_GPU},
+        {"CPU", CPU},
     };
     auto const iter = method_map.find(method_name);
     if (iter == method_map.end()) return std::nullopt;
     return run(iter->second);
 }
 
-// The naive CPU sweep + comparison of stencil.cpp:75-151, generalised to the
-// engine's dims/shapes.  Naive order always (it is the reference's checker),
-// absolute tolerance 1e-4, first mismatch printed in the reference's format.
+// The naive CPU sweep of stencil.cpp:77-131 (check_result's loop), generalised
+// to the engine's dims/shapes: `iterations` sweeps ping-ponging a -> b -> a
+// ...; returns true when the final grid is in b (stencil.cpp:88-92,134).
+// Naive order always (it is the reference's checker and its CPU path).
 template <class T>
-bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const {
-    BoundaryGrid<T> in, out;
-    init_typed(in, out);
+bool Stencil::naive_sweeps(BoundaryGrid<T>& a, BoundaryGrid<T>& b, unsigned iterations) const {
+    BoundaryGrid<T>* in = &a;
+    BoundaryGrid<T>* out = &b;
     const int r = int(options.radius);
-    const int64_t sx = in.row_stride(), sxy = sx * in.rows_with_boundary();
+    const int64_t sx = a.row_stride(), sxy = sx * a.rows_with_boundary();
     T avg;
     if (options.box) {
         int64_t w = 2 * r + 1, n = w * w * (options.dims == 3 ? w : 1);
@@ -273,22 +276,22 @@ bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& 
         avg = T(1) / T(2 * options.dims * r);  // stencil.cpp:85-86
     }
     bool swapped = false;
-    for (unsigned i = 0; i != options.iterations; ++i) {
-        T* src = in.data();
-        T* dst = out.data();
-        for (int64_t z = 0; z < in.depth(); ++z)
-            for (int64_t y = 0; y < in.height(); ++y)
-                for (int64_t x = 0; x < in.width(); ++x) {
+    for (unsigned i = 0; i != iterations; ++i) {
+        T* src = in->data();
+        T* dst = out->data();
+        for (int64_t z = 0; z < in->depth(); ++z)
+            for (int64_t y = 0; y < in->height(); ++y)
+                for (int64_t x = 0; x < in->width(); ++x) {
                     const int64_t zr = options.dims == 3 ? r : 0;
-                    const int64_t c = ((z + zr) * in.rows_with_boundary() + (y + r)) * sx + (x + r);
+                    const int64_t c = ((z + zr) * in->rows_with_boundary() + (y + r)) * sx + (x + r);
                     T sum = T(0);
                     if (options.box) {
                         // separable partial sums (no reference code):
                         // 3D (P(-r) + .. + P(r)) - centre, 2D W + E
                         auto rowsum = [&](int64_t q) {
-                            T a = src[q - r];
-                            for (int dx = -r + 1; dx <= r; ++dx) a += src[q + dx];
-                            return a;
+                            T acc = src[q - r];
+                            for (int dx = -r + 1; dx <= r; ++dx) acc += src[q + dx];
+                            return acc;
                         };
                         if (options.dims == 3) {
                             for (int dz = -r; dz <= r; ++dz) {
@@ -322,6 +325,31 @@ bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& 
         std::swap(in, out);
         swapped = !swapped;
     }
+    return swapped;
+}
+
+// The method CPU: the reference's own CPU path (check_result's naive loop,
+// stencil.cpp:77-131) as a timed method on the host, single-threaded like the
+// reference; the final grid lands where the parity rule puts it.
+template <class T>
+auto Stencil::run_cpu(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std::chrono::steady_clock::duration {
+    initialize_matrix();
+    auto const start = std::chrono::steady_clock::now();
+    naive_sweeps(matrix, result, options.iterations);
+    auto const end = std::chrono::steady_clock::now();
+    device_ms = std::chrono::duration<double, std::milli>(end - start).count();
+    return end - start;
+}
+
+// check_result (stencil.cpp:75-151): the naive CPU sweep from a fresh initial
+// condition, compared with the method's final grid; absolute tolerance 1e-4,
+// first mismatch printed in the reference's format.
+template <class T>
+bool Stencil::check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const {
+    BoundaryGrid<T> ga, gb;
+    init_typed(ga, gb);
+    const bool swapped = naive_sweeps(ga, gb, options.iterations);
+    const BoundaryGrid<T>& in = swapped ? gb : ga;
     const BoundaryGrid<T>& compared = swapped ? result : matrix;
     for (int64_t z = 0; z < in.depth(); ++z)
         for (int64_t y = 0; y < in.height(); ++y)

@@ -32,6 +32,7 @@ public:
         HIP_TEMPORALK,      ///< naive order, 3 or 4 fused time steps per launch (7-point star)
         HIP_PERSISTENT,     ///< naive order, the whole 2D job in one launch (neighbour flags)
         HIP_MULTI_GPU,      ///< naive order, 3D z-slabs over --gpus GPUs, halos over RCCL (stencil_slab_*)
+        CPU,                ///< the reference's CPU path: check_result's naive loop, timed, on the host
     };
 
     Stencil() = default;
@@ -67,6 +68,10 @@ private:
     auto run_slabs(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std::chrono::steady_clock::duration;
     template <class T>
     bool check_typed(const BoundaryGrid<T>& matrix, const BoundaryGrid<T>& result) const;
+    template <class T>
+    bool naive_sweeps(BoundaryGrid<T>& a, BoundaryGrid<T>& b, unsigned iterations) const;
+    template <class T>
+    auto run_cpu(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) -> std::chrono::steady_clock::duration;
     template <class T>
     void init_typed(BoundaryGrid<T>& matrix, BoundaryGrid<T>& result) const;
     template <class T>

@@ -70,3 +70,15 @@ def test_help_lists_reference_flags():
     for flag in ("-s,--matrix-size", "-i,--iteration", "-b,--block-size", "-r,--radius", "-R,--repeat",
                  "-m,--methods", "-c,--check-result"):
         assert flag in out
+
+
+def test_cli_cpu_method_runs_on_the_host():
+    """The CPU method (the reference's check_result loop, timed like a
+    method): the reference's stdout lines, -c passes, no GPU."""
+    import re
+    p = subprocess.run([CLI, "-s", "64", "-b", "8", "-i", "10", "-r", "1", "-m", "CPU", "-c"], capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert "The results of method CPU is correct." in p.stdout
+    assert re.search(r"The average time taken by (.*) method is (.*)ms for \d+ iterations\.", p.stdout).group(1) == "CPU"
+    assert "[stencil-amd] CPU: host" in p.stdout
