@@ -637,6 +637,58 @@ def test_c5_slab_reference_job_against_oracle(gpu):
     assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8))
 
 
+def test_c5_as_benched_whole_2048_cube(gpu):
+    """BASELINE config 5 as bench.py --config C5 runs it on ONE GPU: the whole
+    2048^3 27-point fp64 box grid through AUTO (prepare(), then K = 4 box
+    strip launches with its z-chunking at 2048 planes), from the reference
+    initial condition.  The oracle cannot sweep 2048^3, so the check is
+    size-independent: the initial condition is z-uniform, so after t sweeps
+    every plane more than t from both z ends equals the middle plane of a
+    (2t + 1)-plane grid and every other plane the plane as far from the same
+    end.  That small grid is checked bitwise against the oracle (whole grid,
+    ghosts included); the big grid's per-plane sums against the small grid's
+    (same plane-sum kernel: bitwise); whole planes near both ends and in the
+    middle, ghost rings included, bitwise against the small grid's; the
+    z-ghost planes untouched."""
+    import torch
+    from stencil_amd import _lib
+    n, it = 2048, 12
+    t = it
+    e = engine(gpu, 3, "fp64", "box", 1, "naive", "auto", n, n, n)
+    assert e.fuse_steps == 4
+    assert e.plan(it) == (3, _lib.KERNEL_TEMPORAL2)
+    e.reset()
+    e.prepare()  # as bench.py: the schedule choice settled first, grid a unchanged
+    fin, _ = e.iterate(it)
+    big_sums = e.plane_sums(fin)
+    gh = e.with_ghosts(fin)  # (n + 2, n + 2, n + 2) strided view
+    zs = [0, 1, t - 1, t, n // 2, n - t - 1, n - t, n - 2, n - 1]
+    planes = {z: gh[z + 1].cpu().numpy() for z in zs}
+    ghosts = [gh[0].cpu().numpy(), gh[n + 1].cpu().numpy()]
+    del e, fin, gh
+    torch.cuda.empty_cache()
+    nzs = 2 * t + 1
+    small = engine(gpu, 3, "fp64", "box", 1, "naive", "auto", n, n, nzs)
+    small.reset()
+    sfin, _ = small.iterate(it)
+    small_sums = small.plane_sums(sfin)
+    small_dense = small.to_numpy(sfin)
+    del small, sfin
+    torch.cuda.empty_cache()
+    p = ob.problem(3, "fp64", "box", 1, "naive", n, n, nzs)
+    want_small = ob.run(p, it, threads=16)
+    assert np.array_equal(small_dense.view(np.uint8), want_small.view(np.uint8))
+    z = np.arange(n)
+    idx = np.where(z < t, z, np.where(z >= n - t, nzs - (n - z), t))
+    assert np.array_equal(big_sums.view(np.uint64), small_sums[idx].view(np.uint64))
+    for zz, plane in planes.items():
+        assert np.array_equal(plane.view(np.uint8), want_small[idx[zz] + 1].view(np.uint8)), zz
+    ghost_plane = want_small[0]  # x-ghost columns 1, everything else 0, never written
+    for g in ghosts:
+        assert np.array_equal(g.view(np.uint8), ghost_plane.view(np.uint8))
+    assert float(want_small[t + 1].max()) > 0.0 and float(want_small[t + 1, 1:-1, 1:-1].min()) == 0.0
+
+
 @pytest.mark.parametrize("cfg", ["C5_slab_box_fp64", "C4_slab_fp64", "C3_fp32_4096sq"])
 def test_full_size_baseline_configs(gpu, cfg):
     """Per-GPU shapes of BASELINE configs 3-5 at full x/y size, bitwise
