@@ -535,11 +535,14 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
     if args.exchange != "nccl" or args.share_device:
         raise SystemExit("under torch.distributed.run the halos go over RCCL between distinct GPUs "
                          "(--exchange nccl, no --share-device); rehearse on one GPU without a launcher")
-    free = torch.cuda.mem_get_info(local)[0] if on_gpu else (1 << 40)
-    plan = slab_plan(args.config, world, free, args.n, args.rolling)
     spec = _slab_spec(args, pre)
     dist.init_process_group("gloo")
     try:
+        # one plan for every rank: the least free HBM of any rank decides
+        # whether slabs keep two grids or roll one
+        free = torch.tensor([torch.cuda.mem_get_info(local)[0] if on_gpu else (1 << 40)], dtype=torch.float64)
+        dist.all_reduce(free, op=dist.ReduceOp.MIN)
+        plan = slab_plan(args.config, world, int(free.item()), args.n, args.rolling)
         uid = [SlabJob.unique_id(lib=lib) if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         if on_gpu:
