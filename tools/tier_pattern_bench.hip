@@ -282,6 +282,123 @@ __global__ void __launch_bounds__(64 * (NW + 1))
     if (badc) atomicAdd(bad, badc);
 }
 
+// The same pipeline WITHOUT a dedicated sync wave (the real K = 4 kernel's
+// 8 waves already hold 253 VGPRs each: no room for a ninth): wave 0 polls,
+// and to keep its loads pipelined it PREFETCHES the flags -- the poll load is
+// issued at step p before the step's ring loads, and read at step p + 1
+// behind the counted vmcnt(RY) the step waits for anyway; only a flag still
+// short then spins (draining wave 0's loads).
+__global__ void __launch_bounds__(64 * NW)
+    tier_w0_march(const double* __restrict__ A, double* __restrict__ B, double* __restrict__ C, uint32_t* prod,
+                  uint32_t* cons, unsigned* bad, unsigned* fail, unsigned* spins, int R, uint32_t epoch) {
+    const bool producer = blockIdx.x < 112;
+    const int t = producer ? blockIdx.x : blockIdx.x - 112;
+    if (t >= TILES) return;
+    const int lane = threadIdx.x, w = threadIdx.y;
+    Rows r;
+    region(t, RING, TY, GX, r);
+    const int bx = t % GX, by = t / GX;
+    // every lane of wave 0 polls a flag (branch-free, so the compiler's
+    // vmcnt bookkeeping stays exact): lanes 0..8 their neighbour's, the rest
+    // (and neighbours off the grid) a flag that is always ahead (index 127)
+    int nb = 127;
+    if (w == 0 && lane < 9) {
+        const int nx = bx + lane % 3 - 1, ny = by + lane / 3 - 1;
+        if (nx >= 0 && nx < GX && ny >= 0 && ny < GY) nb = ny * GX + nx;
+    }
+    const uint32_t base = epoch * uint32_t(N);
+    __shared__ double sink[64 * NW];
+    double ring[4][RY];
+    unsigned badc = 0, spin = 0;
+    uint32_t pv = 0;  // the prefetched flag of this lane's neighbour
+    uint32_t* const watched = producer ? cons : prod;
+    auto check_flag = [&](uint32_t need) {  // wave 0: the prefetched value, else spin on fresh polls
+        if (pv < need) {
+            ++spin;
+            wait_ge(watched + nb * FLAG_STRIDE, need, fail);
+        }
+    };
+    auto prefetch_flag = [&] { pv = poll_ld(watched + nb * FLAG_STRIDE); };
+    if (producer) {
+        auto load = [&](double(&d)[RY], int z) {
+            const int zz = z < -1 ? -1 : (z > N ? N : z);
+#pragma unroll
+            for (int k = 0; k < RY; ++k) d[k] = A[ORIGIN + zz * PLANE + r.off[k]];
+        };
+        load(ring[0], -4);
+        load(ring[1], -3);
+        double acc = 0;
+        auto step = [&](auto S_, int p) {
+            constexpr int S = decltype(S_)::value;
+            const int zo = p - K;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RY) : "memory");
+            if (w == 0) check_flag(base + uint32_t(zo >= R ? zo - R + 1 : 0));
+            __syncthreads();
+            if (w == 0 && lane == 0 && zo - 1 >= 0 && zo - 1 < N) flag_st(prod + t * FLAG_STRIDE, base + uint32_t(zo));
+            if (zo >= 0 && zo < N) {
+                double* slot = B + long(zo % R) * PLANE + PORIGIN;
+#pragma unroll
+                for (int k = 0; k < RY; ++k)
+                    if (r.st[k]) sc1_st(slot + r.off[k], double(zo) + 0.0 * ring[(S + 2) % 4][k]);
+            }
+            acc += ring[S][0];
+            if (w == 0) prefetch_flag();
+            load(ring[(S + 2) % 4], p + 2);
+        };
+        for (int p = -4; p + 3 <= N + K; p += 4) {
+            step(std::integral_constant<int, 0>{}, p);
+            step(std::integral_constant<int, 1>{}, p + 1);
+            step(std::integral_constant<int, 2>{}, p + 2);
+            step(std::integral_constant<int, 3>{}, p + 3);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (w == 0 && lane == 0) flag_st(prod + t * FLAG_STRIDE, base + uint32_t(N));
+        sink[w * 64 + lane] = acc;
+        if (spin && lane == 0 && w == 0) atomicAdd(spins, spin);
+        return;
+    }
+    auto load = [&](double(&d)[RY], int z) {  // branch-free: the slot, or the grid's fixed z-ghost plane
+        const bool ghost = z < 0 || z >= N;
+        const double* src = ghost ? A + ORIGIN + long(z < 0 ? -1 : N) * PLANE : B + long((z < 0 ? 0 : z) % R) * PLANE + PORIGIN;
+#pragma unroll
+        for (int k = 0; k < RY; ++k) d[k] = sc1_ld(src + r.off[k]);
+    };
+    load(ring[0], -4);
+    load(ring[1], -3);
+    double acc = 0;
+    auto step = [&](auto S_, int p) {
+        constexpr int S = decltype(S_)::value;
+        const int zo = p - K;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RY) : "memory");
+#pragma unroll
+        for (int k = 0; k < RY; ++k) badc += (p >= 0 && p < N && r.in[k] && ring[S][k] != double(p)) ? 1u : 0u;
+        if (w == 0) check_flag(base + uint32_t(p + 3 < 1 ? 0 : (p + 3 > N ? N : p + 3)));
+        __syncthreads();
+        if (w == 0 && lane == 0 && p >= 0 && p < N) flag_st(cons + t * FLAG_STRIDE, base + uint32_t(p + 1));
+        if (zo >= 0 && zo < N) {
+#pragma unroll
+            for (int k = 0; k < RY; ++k)
+                if (r.st[k]) __builtin_nontemporal_store(ring[(S + 2) % 4][k], C + ORIGIN + zo * PLANE + r.off[k]);
+        }
+        acc += ring[S][0];
+        if (w == 0) prefetch_flag();
+        load(ring[(S + 2) % 4], p + 2);
+    };
+    for (int p = -4; p + 3 <= N + K; p += 4) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w == 0 && lane == 0) flag_st(cons + t * FLAG_STRIDE, base + uint32_t(N));
+    sink[w * 64 + lane] = acc;
+    if (badc) atomicAdd(bad, badc);
+    if (spin && lane == 0 && w == 0) atomicAdd(spins, spin);
+}
+
 // ------------------------------------------------------------------ yshare
 // 64 x 56 regions, x ring 4 (56 written), no y ring (56 rows written); per
 // plane step each workgroup stores its 4 top and 4 bottom rows into an
@@ -436,6 +553,28 @@ int main(int argc, char** argv) {
     std::printf("tier hand-off check: %u stale cells over %u launches (%.3g cells read per launch), %u waits gave up\n",
                 badh[0], epoch, double(TILES) * 64 * RY * NW * (N + 8), badh[1]);
     std::fflush(stdout);
+    // the wave-0 variant on fresh flags / slots
+    CK(hipMemset(prod, 0, 128 * FLAG_STRIDE * 4));
+    CK(hipMemset(cons, 0, 128 * FLAG_STRIDE * 4));
+    CK(hipMemset(slots, 0xff, long(R) * PLANE * 8 + 64 * 8));
+    CK(hipMemset(bad, 0, 16));
+    {  // flag 127 (lanes without a neighbour poll it): always far ahead
+        std::vector<uint32_t> hi(FLAG_STRIDE, 0xF0000000u);
+        CK(hipMemcpy(prod + 127 * FLAG_STRIDE, hi.data(), FLAG_STRIDE * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(cons + 127 * FLAG_STRIDE, hi.data(), FLAG_STRIDE * 4, hipMemcpyHostToDevice));
+    }
+    uint32_t epoch0 = 0;
+    std::snprintf(name, sizeof name, "tier, wave-0 prefetched polls, R=%d", R);
+    timeit(name, 8, [&] {
+        hipLaunchKernelGGL(tier_w0_march, dim3(224), dim3(64, NW), 0, 0, a, slots, c, prod, cons, bad, bad + 1, bad + 3,
+                           R, epoch0);
+        ++epoch0;
+    });
+    CK(hipMemcpy(badh, bad, 16, hipMemcpyDeviceToHost));
+    std::printf("tier wave-0: %u stale cells over %u launches, %u waits gave up, %u spins (flag short when read)\n",
+                badh[0], epoch0, badh[1], badh[3]);
+    std::fflush(stdout);
+    CK(hipMemset(bad, 0, 16));
     uint32_t yepoch = 0;
     timeit("yshare: 64x56 -> 56x56, y rows by hand-off, 2 z-ch", 4, [&] {
         hipLaunchKernelGGL(yshare_march, dim3(YTILES * 2), dim3(64, NW + 1), 0, 0, a, b, xb, stepf, N / 2, yepoch, bad + 2);
