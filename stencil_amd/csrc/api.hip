@@ -153,6 +153,15 @@ int iterate_box_steps(const stencil_problem& p) {
     return steps == 3 || steps == 4 ? steps : 0;
 }
 
+// The two-tier 7-point launch (8 sweeps, kernels_strip.hip TIER; DESIGN.md
+// §9.1f) where the grid's tiles fit twice on the device: STENCIL_TK_TIER=1
+// (experiment, debug library) until measured faster.
+bool iterate_tier(const stencil_layout& l) {
+    if (iterate_tk_steps(l.prob) != 4 || l.prob.dtype != STENCIL_F64) return false;
+    if (knob("STENCIL_TK_TIER", 0) != 1) return false;
+    return tier_eligible(l);
+}
+
 // 2D problems iterate K sweeps per launch with the tile resident in LDS
 // (kernels_tb2d.hip) unless a single-sweep family is forced.
 bool iterate_tb2d(const stencil_problem& p) {
@@ -614,13 +623,18 @@ int stencil_plan(const stencil_layout* l, uint32_t iterations, int64_t* launches
     const int64_t kb = iterate_box_steps(l->prob);
     const int64_t k = kb ? kb : iterate_tk_steps(l->prob);
     int64_t n = iterations;
+    int64_t tier = 0;  // two-tier launches of 8 sweeps
+    if (iterate_tier(*l)) {
+        tier = n / 8;
+        n %= 8;
+    }
     if (k) {
         const int64_t r = n % k;
         n = n / k + r / 2 + r % 2;
     } else if (t2) {
         n = n / 2 + n % 2;
     }
-    if (launches) *launches = n;
+    if (launches) *launches = n + tier;
     if (kernel) *kernel = (k && !kb) ? STENCIL_KERNEL_TEMPORALK : t2 || kb ? STENCIL_KERNEL_TEMPORAL2 : sweep_family(l->prob);
     return STENCIL_OK;
 }
@@ -686,6 +700,25 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
             rc = launch_tb2d(*l, in, out, int(n2), s);
             std::swap(in, out);
             i += n2;
+        }
+    }
+    if (rc == STENCIL_OK && iterations - i >= 8 && iterate_tier(*l)) {
+        TierJob tj;
+        rc = tier_begin(*l, s, &tj);
+        if (rc == STENCIL_EUNSUPPORTED) {  // the device's buffer is in use: K = 4 launches below
+            rc = STENCIL_OK;
+            clear_error();
+        } else {
+            for (; i + 8 <= iterations && rc == STENCIL_OK; i += 8) {
+                rc = tier_launch(*l, in, out, &tj, s);
+                std::swap(in, out);
+            }
+            bool failed = false;
+            const int rc2 = tier_end(&tj, s, &failed);
+            if (rc == STENCIL_OK) rc = rc2;
+            if (rc == STENCIL_OK && failed)
+                rc = set_error(STENCIL_EHIP, "two-tier launch: a plane hand-off wait gave up (were the workgroups "
+                                             "not all resident -- another job on the GPU?); the grid is wrong");
         }
     }
     if (const uint32_t k = uint32_t(iterate_tk_steps(l->prob))) {

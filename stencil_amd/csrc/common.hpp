@@ -133,6 +133,24 @@ int launch_zmarch(const stencil_layout& l, const void* in, void* out, int64_t be
                   hipStream_t s);
 int launch_temporal2(const stencil_layout& l, const void* in, void* out, int64_t begin,
                      int64_t end, hipStream_t s);
+// The two-tier 7-point launch (kernels_strip.hip TIER): 8
+// sweeps per launch, the intermediate grid through a ring of plane slots.
+struct TierJob {
+    void* mem = nullptr;  // slots + flags + fail counter (stream-ordered allocation)
+    int64_t tiles = 0;
+    struct Args {
+        void* slots = nullptr;
+        uint32_t* prod = nullptr;
+        uint32_t* cons = nullptr;
+        unsigned* fail = nullptr;
+        uint32_t base = 0;
+        int rmask = 0;
+    } a;
+};
+bool tier_eligible(const stencil_layout& l);
+int tier_begin(const stencil_layout& l, hipStream_t s, TierJob* j);
+int tier_launch(const stencil_layout& l, const void* in, void* out, TierJob* j, hipStream_t s);
+int tier_end(TierJob* j, hipStream_t s, bool* failed);
 int launch_temporalk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end,
                      int steps, hipStream_t s);
 int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,

@@ -105,6 +105,66 @@ struct StripTile {
     static constexpr size_t lds_bytes = size_t(NB) * K * NW * 2 * RW * sizeof(T);
 };
 
+// TIER (the two-tier job): a launch of 2 x tiles
+// workgroups does 2K sweeps.  Workgroups [0, tiles) are PRODUCERS: the K-step
+// march of their tile over the whole z range, storing t_K (the grid after K
+// sweeps) -- output tile plus the region's ghost cells -- into a ring of R
+// plane slots instead of the output grid.  Workgroups [tiles, 2 tiles) are
+// CONSUMERS: the same march over the slots (their neighbours' outputs give the
+// region's ring; the fixed z-ghost planes come from `in`), storing t_2K to
+// `out`.  Only `in` and `out` travel to HBM; the slots (R x one plane) stay in
+// the Infinity Cache.  Hand-off per plane (MI355X_MICROARCH.md, inter-workgroup
+// visibility, hand-off table row 1): slot stores and loads are `sc1`; a
+// producer publishes "planes stored" once every wave's counted vmcnt shows its
+// stores of the previous step done and a barrier has joined the waves; a
+// consumer publishes "planes loaded" the same way; a consumer's wave 0 checks
+// its <= 9 producers before the step that loads a plane, a producer's its <= 9
+// consumers before reusing a slot.  The checks read flags PREFETCHED one step
+// earlier (issued before that step's plane loads, so the counted wait the step
+// does anyway covers them -- wave 0's loads stay pipelined); only a flag still
+// short spins, with a budget: a wait that gives up counts in `fail` and the
+// host reports the job as failed.  All 2 x tiles workgroups must be resident
+// at once (one per CU): the host launches it only when they fit.
+// (TierJob::Args, common.hpp): slots = R plane slots in the grid's plane
+// layout (plane z -> slot z & rmask, R a power of two); prod / cons = per
+// tile, one 128-B line each, the planes stored / loaded by every wave (+ base,
+// this launch's flag origin: flags run on across launches); fail = waits
+// that gave up
+using TierArgs = TierJob::Args;
+constexpr int kTierFlagStride = 32;  // uint32 per flag line
+
+__device__ __forceinline__ uint32_t tier_poll(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tier_publish(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool tier_ge(uint32_t a, uint32_t b) { return int32_t(a - b) >= 0; }
+// spin until *p >= need (wrap-safe), a tenth of a second at most; once any
+// wait of the launch has given up, every later one returns at once, so a
+// broken hand-off ends the launch quickly (with a wrong grid the host reports)
+__device__ __forceinline__ void tier_spin(const uint32_t* p, uint32_t need, unsigned* fail) {
+    for (int it = 0; !tier_ge(tier_poll(p), need); ++it) {
+        if (it > (1 << 22) || (it % 1024 == 0 && tier_poll(fail) != 0)) {
+            atomicAdd(fail, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+template <typename VT>
+__device__ __forceinline__ VT sc1_load(const void* p) {
+    static_assert(sizeof(VT) == 8, "tier hand-offs move 8-byte lane vectors");
+    return __builtin_bit_cast(VT, __hip_atomic_load(static_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT));
+}
+template <typename VT>
+__device__ __forceinline__ void sc1_store(void* p, const VT& v) {
+    static_assert(sizeof(VT) == 8, "tier hand-offs move 8-byte lane vectors");
+    __hip_atomic_store(static_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // DIAG (timing experiments only, results are wrong): 1 = no loads after the
 // first two planes, 2 = no arithmetic (t_s = centre), 3 = no stores
 // SIG: face signalling for multi-GPU slabs (stencil_sweepk_signal): the
@@ -126,11 +186,12 @@ struct StripTile {
 // for 7 ds_write_b64 + 28 ds_read_b64 per wave and step, which pays for one
 // more fused sweep (K = 5) at the same 7-row strips.
 template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true,
-          bool HL = false>
+          bool HL = false, bool TIER = false>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
-                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast, int xcd_pw) {
+                unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast, int xcd_pw,
+                TierArgs tier) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -150,7 +211,13 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t tiles = int64_t(tiles_x) * tiles_y;
     int64_t lo, hi;
     bool rev = false;  // this workgroup's chunk marches down (SIG: the last chunk)
-    if (sched) {
+    static_assert(!TIER || (!SIG && sizeof(T) * V == 8), "TIER: plain launches of 8-byte lane vectors");
+    const bool tprod = TIER && int64_t(blockIdx.x) < tiles;  // TIER: producer (else consumer)
+    if constexpr (TIER) {  // one segment per workgroup: its tile, the whole z range
+        const int64_t t = tprod ? int64_t(blockIdx.x) : int64_t(blockIdx.x) - tiles;
+        lo = t * nzr;
+        hi = lo + nzr;
+    } else if (sched) {
         // packed schedule (STENCIL_TK_PACK): {tile, first plane, planes}; on
         // face-signalled launches planes < 0 marks the chunk that ends at the
         // top face and marches down (packed_schedule's faces_out tables)
@@ -205,8 +272,10 @@ __global__ void __launch_bounds__(64 * NW)
     // neighbour strips (the first / last wave reads its own: those rows are ring rows)
     const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
 
-    auto segment = [&](auto REV_) {  // one segment: tile t, planes [za, zb)
+    auto segment = [&](auto REV_, auto PROD_) {  // one segment: tile t, planes [za, zb)
     constexpr bool REV = decltype(REV_)::value;
+    constexpr bool PROD = TIER && decltype(PROD_)::value;  // TIER producer (stores t_K into the slots)
+    constexpr bool CONS = TIER && !PROD;                   // TIER consumer (reads the slots)
     const int t = int(lo / nzr);
     const int za = zbeg + int(lo - int64_t(t) * nzr);
     const int zb = za + (hi - lo < int64_t(zend - za) ? int(hi - lo) : zend - za);
@@ -237,6 +306,26 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
+    // TIER producer: the slot cells this lane stores per row -- its output
+    // tile's, and the region's ghost cells (x in {-1, nx} or y in {-1, ny}:
+    // ghost cells never change, and the consumers' regions read them from the
+    // slots); V = 1
+    // (ghost cells: x in {-1, nx} with y in [-1, ny], or y in {-1, ny} with x
+    // in [-1, nx]; the x part per lane, the y part per row, uniform)
+    const bool xghost = PROD && (x == -1 || x == g.nx);
+    const bool xspan = PROD && x >= -1 && x <= g.nx;
+    int tnb = -1;  // TIER: the neighbour tile (3 x 3, lanes 0..8 of wave 0) whose flag this lane watches
+    if constexpr (TIER) {
+        const int nbx = bx + lane % 3 - 1, nby = by + lane / 3 - 1;
+        if (w == 0 && lane < 9 && nbx >= 0 && nbx < tiles_x && nby >= 0 && nby < tiles_y) tnb = nby * tiles_x + nbx;
+    }
+    uint32_t* const tier_mine = TIER ? (PROD ? tier.prod : tier.cons) + int64_t(t) * kTierFlagStride : nullptr;
+    const uint32_t* const tier_flags = TIER ? (PROD ? tier.cons : tier.prod) : nullptr;  // + the watched tile's line
+    // slot z's plane base (biased like src / dst)
+    const char* const slots = TIER ? static_cast<const char*>(tier.slots) +
+                                         (g.origin - (g.origin / plane) * plane - bias) * int64_t(sizeof(T))
+                                   : nullptr;
+    uint32_t tier_pv = 0;  // the prefetched flag
     // the whole region inside the grid in x and y: intermediate stages need no
     // ghost-cell select on steps whose stage planes are all inside in z
     const bool xy_inner = fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
@@ -254,11 +343,32 @@ __global__ void __launch_bounds__(64 * NW)
     auto load_plane = [&](VT (&d)[RY], int m) {
         const int z = zr(m);
         const int zz = z < zfirst ? zfirst : (z > zlast ? zlast : z);
+        if constexpr (CONS) {
+            // consumer: every plane from the slots (sc1): plane z in slot z & rmask,
+            // the fixed z-ghost planes -1 / nz in slots R / R + 1
+            const int slot = zz < 0 ? tier.rmask + 1 : (zz >= nz ? tier.rmask + 2 : (zz & tier.rmask));
+            const char* base = slots + int64_t(slot) * plane * int64_t(sizeof(T));
+#pragma unroll
+            for (int k = 0; k < RY; ++k) d[k] = sc1_load<VT>(base + off[k]);
+            return;
+        }
         const char* base = src + int64_t(zz) * plane * int64_t(sizeof(T));
 #pragma unroll
         for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(base + off[k]);
     };
 
+    // TIER producer: one plane's output-tile and ghost cells into a slot
+    auto tier_store_plane = [&](const VT (&d)[RY], int slot) {
+        if constexpr (PROD) {
+            char* base = const_cast<char*>(slots) + int64_t(slot) * plane * int64_t(sizeof(T));
+#pragma unroll
+            for (int k = 0; k < RY; ++k) {
+                const int64_t y = y0 + k;
+                const bool yghost = y == -1 || y == g.ny, yspan = y >= -1 && y <= g.ny;
+                if ((st[k] && xin[0]) || (yghost && xspan) || (xghost && yspan)) sc1_store<VT>(base + off[k], d[k]);
+            }
+        }
+    };
     static_assert(NS >= 4, "the input ring holds in(p-2) .. in(p+1) at least");
     constexpr int LCM = NS % 2 == 0 ? NS : 2 * NS;  // steps until ring slot and H parity repeat
     const int p0 = za - K;
@@ -283,8 +393,18 @@ __global__ void __launch_bounds__(64 * NW)
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int k = 0; k < RY; ++k) H[s][b][k] = VT{};
+    if constexpr (CONS) {
+        // the first loads read slot R (the bottom z-ghost plane): wait until
+        // every producer in reach has stored it (and plane 0)
+        if (tnb >= 0) tier_spin(tier_flags + tnb * kTierFlagStride, tier.base + 1u, tier.fail);
+        __syncthreads();
+    }
 #pragma unroll
     for (int i = 0; i < NS - 2; ++i) load_plane(vin[i], p0 + i);
+    if constexpr (PROD) {  // the bottom z-ghost plane (p0 clamps to -1) into slot R
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tier_store_plane(vin[0], tier.rmask + 1);
+    }
 
 
     auto stepb = [&](auto S_, int p, auto FAST_) {
@@ -292,7 +412,27 @@ __global__ void __launch_bounds__(64 * NW)
         constexpr bool FAST = decltype(FAST_)::value;  // no ghost-cell selects this step
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
         constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
+        if constexpr (TIER) {
+            // this step's input plane and the previous step's stores are done
+            // (only plane p+1's RY loads, issued after them, may be in flight);
+            // the flag prefetched last step is then in too
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RY) : "memory");
+            if (tnb >= 0) {
+                // producer: slot of plane p-K free (its consumers loaded plane
+                // p-K-R); consumer: plane p+2, loaded at the end of this step, stored
+                const int need = PROD ? p - K - tier.rmask : (p + 3 <= nz ? p + 3 : nz + 1);
+                if (need > 0 && !tier_ge(tier_pv, tier.base + uint32_t(need)))
+                    tier_spin(tier_flags + tnb * kTierFlagStride, tier.base + uint32_t(need), tier.fail);
+            }
+        }
         __syncthreads();  // boundary rows of step p-1 are visible
+        if constexpr (TIER) {
+            // every wave's wait above is behind the barrier: publish the planes
+            // stored (producer: t_K up to p-K-1) / loaded (consumer: up to p)
+            const int done = PROD ? p - K : p + 1;
+            if (threadIdx.x == 0 && threadIdx.y == 0 && done > 0 && done <= nz)
+                tier_publish(tier_mine, tier.base + uint32_t(done));
+        }
         // Row-major order: for each row k all K stages, so only one result per
         // stage is live at a time (stage s+1 of row k needs stage s of row k
         // only as z+; its y-neighbours are the previous step's planes in H).
@@ -346,6 +486,8 @@ __global__ void __launch_bounds__(64 * NW)
                     sum += REV ? zm[j] : zp[j];
                     o[j] = DIAG == 2 ? c[j] : sfma0(sum, avg);
                     if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
+                    // TIER producer: t_K keeps the ghost cells too (they go to the slots)
+                    if (PROD && s == K && !FAST) o[j] = (yin[k] && xin[j]) ? o[j] : c[j];
                 }
                 // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
                 if constexpr (s >= 2) hset(s - 1, (S - s + 5) & 1, k, prev);
@@ -358,6 +500,14 @@ __global__ void __launch_bounds__(64 * NW)
             if constexpr (K >= 5) stage(std::integral_constant<int, (K >= 5 ? 5 : 1)>{});
             if constexpr (K >= 6) stage(std::integral_constant<int, (K >= 6 ? 6 : 1)>{});
             static_assert(K >= 2 && K <= 6, "K = 2..6");
+            if constexpr (PROD) {
+                const int64_t y = y0 + k;
+                const bool yghost = y == -1 || y == g.ny, yspan = y >= -1 && y <= g.ny;
+                if (do_store && ((st[k] && xin[0]) || (yghost && xspan) || (xghost && yspan)))
+                    sc1_store<VT>(const_cast<char*>(slots) + int64_t(zo & tier.rmask) * plane * int64_t(sizeof(T)) +
+                                      off[k], prev);
+                continue;
+            }
             if (do_store && st[k]) {
                 T* q = reinterpret_cast<T*>(obase + off[k]);
                 if (xst[V - 1]) {
@@ -409,6 +559,9 @@ __global__ void __launch_bounds__(64 * NW)
                 }
             }
         }
+        if constexpr (TIER) {  // read at the next step, behind its counted wait
+            if (tnb >= 0) tier_pv = tier_poll(tier_flags + tnb * kTierFlagStride);
+        }
         if constexpr (DIAG != 1) load_plane(vin[(S + NS - 2) % NS], p + NS - 2);  // slot of in(p-2), consumed above
     };
     auto step = [&](auto S_, int p) {
@@ -433,13 +586,28 @@ __global__ void __launch_bounds__(64 * NW)
     int p = p0;
     for (; p + LCM - 1 <= plast; p += LCM) unroll_steps<0, LCM>(step, p);
     tail_steps<0, LCM - 1>(step, p, plast);
+    if constexpr (TIER) {
+        if constexpr (PROD) {
+            // the top z-ghost plane into slot R + 1: the ring's last loads
+            // were clamped to plane nz
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tier_store_plane(vin[0], tier.rmask + 2);
+        }
+        // the last stores / loads are done: the whole range (+ the ghost slot)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0 && threadIdx.y == 0) tier_publish(tier_mine, tier.base + uint32_t(nz + 1));
+    }
     };  // segment
     while (lo < hi) {
-        if constexpr (SIG) {
-            if (rev) segment(std::true_type{});
-            else segment(std::false_type{});
+        if constexpr (TIER) {
+            if (tprod) segment(std::false_type{}, std::true_type{});
+            else segment(std::false_type{}, std::false_type{});
+        } else if constexpr (SIG) {
+            if (rev) segment(std::true_type{}, std::false_type{});
+            else segment(std::false_type{}, std::false_type{});
         } else {
-            segment(std::false_type{});
+            segment(std::false_type{}, std::false_type{});
         }
     }
 }
@@ -568,7 +736,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
                            static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
                            int(gy), int(lo), int(hi), avg_weight<T>(l.prob), sig, fsig, packed ? sched : nullptr,
-                           fast_of(packed), packed ? 0 : xcd_pw);
+                           fast_of(packed), packed ? 0 : xcd_pw, TierArgs{});
         return hipGetLastError();
     };
     if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
@@ -577,7 +745,138 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     return STENCIL_OK;
 }
 
+// ---- the two-tier launch (TIER, above): host side --------------------------
+#ifndef STRIP_ILP_TU
+using TierKernelShape = StripTile<double, 1, 7, 8, 4, true>;
+constexpr int kTierSlots = 16;  // R: plane slots of the producer -> consumer ring (2.2 MB each at 512^2 fp64)
+
+int tier_tiles(const stencil_layout& l, int64_t* tiles) {
+    const Geom g = geom_of(l);
+    *tiles = ((g.nx + TierKernelShape::TX - 1) / TierKernelShape::TX) * ((g.ny + TierKernelShape::TY - 1) / TierKernelShape::TY);
+    return STENCIL_OK;
+}
+#endif
+
 }  // namespace
+
+#ifndef STRIP_ILP_TU
+// Can the grid run the two-tier launch?  The fp64 7-point star, K = 4 strip
+// shape, a single grid (no slab halos), at least 2K planes, and both tiers'
+// workgroups resident at once (2 x tiles <= the device's workgroup slots).
+bool tier_eligible(const stencil_layout& l) {
+    if (l.prob.dtype != STENCIL_F64 || !temporal2_supports(l.prob)) return false;
+    if (l.prob.flags & (STENCIL_HALO_LO | STENCIL_HALO_HI)) return false;
+    if (l.prob.nz < 8 || l.prob.nx < 1 || l.prob.ny < 1) return false;
+    int64_t tiles = 0;
+    tier_tiles(l, &tiles);
+    int slots = 0;
+    if (resident_slots(tkstrip_7pt<double, 1, 7, 8, 4, true, 0, false, 4, false, true, true>, 64 * 8, &slots) !=
+        STENCIL_OK)
+        return false;
+    return 2 * tiles <= slots;
+}
+
+// The slots + flags live in one device buffer per GPU, kept for the process
+// (allocated on first use, grown when a larger plane needs it) and held by
+// one job at a time: a job that finds it taken (another stream of the same
+// process in the middle of a two-tier job) gets STENCIL_EUNSUPPORTED and the
+// caller runs the K = 4 launches instead.
+namespace {
+struct TierBuffer {
+    void* mem = nullptr;
+    size_t bytes = 0;
+    bool busy = false;
+};
+std::mutex g_tier_mu;
+std::map<int, TierBuffer> g_tier_buf;
+}  // namespace
+
+int tier_begin(const stencil_layout& l, hipStream_t s, TierJob* j) {
+    *j = TierJob{};
+    int64_t tiles = 0;
+    tier_tiles(l, &tiles);
+    // R slots for the ring + 2 for the fixed z-ghost planes
+    const size_t slot_bytes = size_t(kTierSlots + 2) * size_t(l.plane) * sizeof(double) + 256;
+    const size_t flag_bytes = size_t(2 * tiles) * kTierFlagStride * sizeof(uint32_t);
+    const size_t bytes = slot_bytes + flag_bytes + 256;
+    int dev = 0;
+    STENCIL_HIP_CHECK(hipGetDevice(&dev));
+    void* mem = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_tier_mu);
+        TierBuffer& b = g_tier_buf[dev];
+        if (b.busy) return set_error(STENCIL_EUNSUPPORTED, "the two-tier buffer of device %d is in use", dev);
+        if (b.bytes < bytes) {
+            if (b.mem) {
+                (void)hipDeviceSynchronize();  // an earlier job's launches may still read it
+                (void)hipFree(b.mem);
+                b.mem = nullptr;
+                b.bytes = 0;
+            }
+            if (hipMalloc(&b.mem, bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                b.mem = nullptr;
+                return set_error(STENCIL_ENOMEM, "two-tier buffer of %zu bytes", bytes);
+            }
+            b.bytes = bytes;
+        }
+        b.busy = true;
+        mem = b.mem;
+    }
+    char* m = static_cast<char*>(mem);
+    if (hipMemsetAsync(m + slot_bytes, 0, flag_bytes + 256, s) != hipSuccess) {
+        std::lock_guard<std::mutex> lock(g_tier_mu);
+        g_tier_buf[dev].busy = false;
+        return set_error(STENCIL_EHIP, "two-tier flag reset failed");
+    }
+    j->mem = mem;
+    j->tiles = tiles;
+    j->a.slots = m;
+    j->a.prod = reinterpret_cast<uint32_t*>(m + slot_bytes);
+    j->a.cons = j->a.prod + tiles * kTierFlagStride;
+    j->a.fail = reinterpret_cast<unsigned*>(m + slot_bytes + flag_bytes);
+    j->a.base = 0;
+    j->a.rmask = kTierSlots - 1;
+    return STENCIL_OK;
+}
+
+// One launch: 2K = 8 sweeps of the whole grid, in -> out.
+int tier_launch(const stencil_layout& l, const void* in, void* out, TierJob* j, hipStream_t s) {
+    const Geom g = geom_of(l);
+    const int64_t gx = (g.nx + TierKernelShape::TX - 1) / TierKernelShape::TX;
+    const int64_t gy = (g.ny + TierKernelShape::TY - 1) / TierKernelShape::TY;
+    if ((g.plane + g.row + 64) * int64_t(sizeof(double)) >= (int64_t(1) << 32) || g.nz >= (int64_t(1) << 30))
+        return set_error(STENCIL_EINVAL, "plane too large for the two-tier launch");
+    auto kern = tkstrip_7pt<double, 1, 7, 8, 4, true, 0, false, 4, false, true, true>;
+    const int fast = 1;  // few tiles: the interior fast path pays (as the packed regime)
+    hipLaunchKernelGGL(kern, dim3(unsigned(2 * j->tiles)), dim3(64, 8, 1), 0, s, static_cast<const double*>(in),
+                       static_cast<double*>(out), g, 0, int(g.nz), 0, int(gx), int(gy), 0, 0,
+                       avg_weight<double>(l.prob), nullptr, nullptr, nullptr, fast, 0, j->a);
+    STENCIL_LAUNCH_CHECK();
+    j->a.base += uint32_t(g.nz + 1);  // the flags end at base + nz + 1: the next launch's origin
+    return STENCIL_OK;
+}
+
+// Free the job's memory (stream-ordered) and report whether any hand-off wait
+// gave up (then the grid is wrong): one host wait on `s`.
+int tier_end(TierJob* j, hipStream_t s, bool* failed) {
+    *failed = false;
+    if (!j->mem) return STENCIL_OK;
+    unsigned f = 0;
+    hipError_t e = hipMemcpyAsync(&f, j->a.fail, sizeof f, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // the job's launches are done: the buffer is free
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lock(g_tier_mu);
+        g_tier_buf[dev].busy = false;
+    }
+    j->mem = nullptr;
+    if (e != hipSuccess) return set_error(STENCIL_EHIP, "two-tier job: %s", hipGetErrorString(e));
+    *failed = f != 0;
+    return STENCIL_OK;
+}
+#endif  // !STRIP_ILP_TU
 
 #ifdef STRIP_ILP_TU
 // kernels_strip_ilp.hip: the two default shapes measured faster when this file is compiled under LLVM's

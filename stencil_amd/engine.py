@@ -79,7 +79,7 @@ class JacobiEngine:
         self.fuse_steps = 1
         if self.fused:
             # sweeps per fused launch: the most sweeps stencil_iterate runs as one launch
-            self.fuse_steps = next((k for k in (5, 4, 3, 2) if self.plan(k)[0] == 1), 2)
+            self.fuse_steps = next((k for k in (8, 5, 4, 3, 2) if self.plan(k)[0] == 1), 2)
         self.slow_extent = int(self.lib.stencil_slow_extent(ctypes.byref(self.layout)))
         # one slow-axis unit = a whole plane (3D) or a whole padded row (2D)
         self.unit = int(self.layout.plane if spec.dims == 3 else self.layout.row)

@@ -11,6 +11,7 @@
 #   bench1000        the default 1000-step C2 bench
 #   prof:<cfg>       profiles/collect.sh (kernel trace + FETCH/WRITE passes) of bench --config <cfg>
 #   tier             tools/tier_pattern_bench 16 and 32 (the C2 decision gate)
+#   tierbench        the C2 bench through the two-tier launches (STENCIL_TK_TIER=1, debug library)
 #   ramp             tools/ramp_probe.py under a rocprofv3 kernel trace (per-launch durations by phase)
 set -o pipefail
 TAG=$1; shift
@@ -39,6 +40,8 @@ for step in "$@"; do
           timeout -k 10 120 tools/tier_pattern_bench 32 > "$O/tier32.txt" 2>&1 ;;
     ramp) (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O/ramp" -o run -- \
              python3 "$R/tools/ramp_probe.py" > "$O/ramp.log" 2>&1) ;;
+    tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
+             --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

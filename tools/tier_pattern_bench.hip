@@ -68,12 +68,12 @@ __device__ __forceinline__ uint32_t poll_ld(const uint32_t* p) {
 __device__ __forceinline__ void flag_st(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Spin until *p >= need, with a budget (~1 s): a wait that gives up bumps
+// Spin until *p >= need, with a budget (~0.1 s): a wait that gives up bumps
 // *fail and returns, so every wave of the grid reaches its end whatever
 // happens (a lost workgroup then shows as wrong tags, never as a hang).
 __device__ __forceinline__ void wait_ge(const uint32_t* p, uint32_t need, unsigned* fail) {
     for (int it = 0; poll_ld(p) < need; ++it) {
-        if (it > (1 << 24)) {
+        if (it > (1 << 22) || (it % 1024 == 0 && poll_ld(fail) != 0)) {  // after one timeout every wait bails
             atomicAdd(fail, 1u);
             return;
         }
