@@ -482,6 +482,34 @@ def _slab_spec(args, pre):
     return StencilSpec(dims=3, dtype=pre["dtype"], shape=pre["shape"], radius=1, order="naive", kernel=args.kernel)
 
 
+SETTLE_MS = 25.0  # as stencil_prepare: the GPU's clock settles over ~15 ms of heavy launches after idling
+
+
+def settle_rounds(job, k, rounds=None):
+    """Untimed rounds for about SETTLE_MS (at most 64 rounds): `rounds` of
+    them, or -- one process -- as many as one timed round says fit; returns
+    the sweeps run (the check counts them).  Ranks of one job must run the
+    same rounds (every round exchanges halos): they pass `rounds` from
+    settle_rounds_for(), which depends only on the global problem."""
+    if rounds is None:
+        ms = job.run(k)
+        n = int(min(64, SETTLE_MS / ms)) if ms > 0 else 0
+        if n:
+            job.run(n * k)
+        return k * (n + 1)
+    if rounds:
+        job.run(rounds * k)
+    return rounds * k
+
+
+def settle_rounds_for(grid, world, k, rate_gcell=1000.0):
+    """The same settle round count on every rank: SETTLE_MS at an assumed
+    rate_gcell per GPU, 1 to 64 rounds."""
+    gnx, gny, gnz = grid
+    round_ms = float(gnx) * gny * gnz / world * k / (rate_gcell * 1e9) * 1e3
+    return int(max(1, min(64, round(SETTLE_MS / max(round_ms, 1e-6)))))
+
+
 def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, barrier=None):
     """The per-rank body of the rank-mode job: build this rank's slab, warm
     up, time exactly args.steps sweeps, time the compute launches of extra
@@ -497,6 +525,9 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
         job.fill_initial(args.init, INIT_SEED)
         sweeps = k + 1 + args.warmup
         job.run(k + 1)  # a full and a remainder round: both launch paths' one-time costs
+        if barrier:
+            barrier()
+        sweeps += settle_rounds(job, k, settle_rounds_for(grid, world, k))  # the same rounds on every rank
         job.run(args.warmup)
         if barrier:
             barrier()
@@ -624,6 +655,7 @@ def main_slab_job(args):
     # the one-time costs of both launch paths (schedule trials, first launches)
     sweeps = k + 1 + args.warmup
     job.run(k + 1)
+    sweeps += settle_rounds(job, k)
     job.run(args.warmup)
     elapsed = job.run(args.steps) * 1e-3  # host wall time, every device synchronised at both ends
     sweeps += args.steps

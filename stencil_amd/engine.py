@@ -169,7 +169,9 @@ class JacobiEngine:
 
     def prepare(self, stream=None) -> None:
         """stencil_prepare: settle the job's one-time per-shape choices (the
-        z-chunk schedule trial) by one fused launch a -> b; `a` is unchanged."""
+        z-chunk schedule trial) by one fused launch a -> b, then the same
+        launch for ~25 ms of device time so the GPU's clock has settled
+        (DESIGN.md §6); `a` is unchanged."""
         _lib.check(self.lib.stencil_prepare(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
                                             ctypes.c_void_p(self.b.data_ptr()), _stream_handle(stream)),
                    "stencil_prepare", lib=self.lib)

@@ -19,13 +19,15 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R" || exit 1
+n=0
 for step in "$@"; do
   echo "[lease] $TAG: $step $(date +%T)"
   case "$step" in
     tests) timeout -k 10 1100 python3 -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests \
              > "$O/gpu_tests.txt" 2>&1 ;;
-    tests:*) timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
-             $(echo "${step#tests:}" | tr ',' ' ') > "$O/gpu_tests_part.txt" 2>&1 ;;
+    tests:*) n=$((n + 1))
+             timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+             $(echo "${step#tests:}" | tr ',' ' ') > "$O/gpu_tests_part$n.txt" 2>&1 ;;
     smoke) timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench.err" ;;
     bench1000) timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline \
