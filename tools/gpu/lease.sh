@@ -9,6 +9,7 @@
 #   bench            the driver's command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   bench:<cfg>      bench.py --config <cfg> (C1..C5, NS) at its usual length
 #   bench1000        the default 1000-step C2 bench
+#   benchr:<cfg>     bench.py --config <cfg> --init random (a developed field)
 #   prof:<cfg>       profiles/collect.sh (kernel trace + FETCH/WRITE passes) of bench --config <cfg>
 #   tier             tools/tier_pattern_bench 16 and 32 (the C2 decision gate)
 #   tierbench        the C2 bench through the two-tier launches (STENCIL_TK_TIER=1, debug library)
@@ -35,6 +36,10 @@ for step in "$@"; do
     bench:*) c=${step#bench:}
              case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
              timeout -k 10 400 python3 bench.py --config "$c" $a > "$O/bench_$c.json" 2>> "$O/bench.err" ;;
+    benchr:*) c=${step#benchr:}   # the same on a developed field (uniform random interior)
+             case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+             timeout -k 10 400 python3 bench.py --config "$c" --init random $a --no-cpu-baseline \
+               > "$O/bench_${c}_random.json" 2>> "$O/bench.err" ;;
     prof:*) c=${step#prof:}
             case "$c" in C5) a="--steps 8 --warmup 0";; *) a="--steps 100 --warmup 5";; esac
             bash profiles/collect.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/collect_$c.log" 2>&1 ;;
