@@ -219,7 +219,9 @@ int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end,
  * stencil_wait_counters queues on `stream` a one-lane kernel that returns
  * when counters[0] >= target_lo and counters[1] >= target_hi -- what is
  * queued behind it (the halo send) waits for the faces, not for the whole
- * launch.  After 10 s it sets *timeout_flag and returns instead.
+ * launch.  After 10 s it sets *timeout_flag and returns instead; a wait that
+ * finds *timeout_flag already set returns at once (a lost peer costs one
+ * timeout, and the slab job's run() reports it).
  * stencil_wait_face_signal queues the same wait on the command processor
  * (hipStreamWaitValue64, *face_signal >= target): no kernel, no timeout. */
 int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,

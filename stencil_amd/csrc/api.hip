@@ -263,9 +263,13 @@ __global__ void __launch_bounds__(256) plane_sums_kernel(const T* __restrict__ b
 // kernels queued behind it on its stream (the RCCL send of the faces) start
 // only then; the producers released before adding.  Gives up after 10 s of
 // s_memrealtime (100 MHz) and sets *timeout instead of holding the queue.
+// The flag is sticky: once a wait has given up, later waits on the same flag
+// return at once, so a lost peer costs one timeout, not one per round (the
+// job's run() then reports the failure).
 __global__ void __launch_bounds__(64) wait_counters_kernel(const uint32_t* __restrict__ c, uint32_t tlo, uint32_t thi,
                                                            uint32_t* __restrict__ timeout) {
     if (threadIdx.x != 0) return;
+    if (__hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         const uint32_t a = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -165,6 +165,28 @@ def test_sweepk_signal_equals_sweepk(gpu, monkeypatch, dtype, steps, zchunk, fla
     assert sig[0].item() == nsig and sig[1].item() == nsig and sig[2].item() == 0 and nsig > 0
 
 
+def test_wait_counters_timeout_flag_is_sticky(gpu):
+    """A wait whose timeout flag is already set (an earlier wait gave up on a
+    lost peer) returns at once instead of spinning another 10 s; a wait whose
+    targets are met returns and leaves the flag as it was."""
+    import time
+    e = JacobiEngine(StencilSpec(dims=3, dtype="fp64"), 16, 16, 8, device=gpu)
+    sig = torch.zeros(4, dtype=torch.int32, device=e.a.device)
+    sig[2] = 1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.wait_counters(sig, 5, 5)  # never met: counters stay 0
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 2.0
+    assert sig.tolist() == [0, 0, 1, 0]
+    sig[2] = 0
+    sig[0] = 3
+    sig[1] = 4
+    e.wait_counters(sig, 3, 4)
+    torch.cuda.synchronize()
+    assert sig.tolist() == [3, 4, 0, 0]
+
+
 @pytest.mark.parametrize("flags", [0, 3])
 @pytest.mark.parametrize("pack_sig", ["1", "0"])
 def test_sweepk_signal_packed_schedule(gpu, monkeypatch, capfd, flags, pack_sig):

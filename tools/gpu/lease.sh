@@ -14,6 +14,7 @@
 #   tier             tools/tier_pattern_bench 16 and 32 (the C2 decision gate)
 #   tierbench        the C2 bench through the two-tier launches (STENCIL_TK_TIER=1, debug library)
 #   ramp             tools/ramp_probe.py under a rocprofv3 kernel trace (per-launch durations by phase)
+#   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
@@ -47,6 +48,9 @@ for step in "$@"; do
           timeout -k 10 120 tools/tier_pattern_bench 32 > "$O/tier32.txt" 2>&1 ;;
     ramp) (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O/ramp" -o run -- \
              python3 "$R/tools/ramp_probe.py" > "$O/ramp.log" 2>&1) ;;
+    c1probe) timeout -k 10 120 python3 tools/c1_probe.py > "$O/c1_probe.txt" 2>&1 &&
+             (cd /tmp && TMPDIR=/tmp timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d "$O/c1trace" \
+               -o run -- python3 "$R/tools/c1_probe.py" --reps 10 > "$O/c1_probe_traced.txt" 2>&1) ;;
     tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
              --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
