@@ -252,11 +252,12 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
  * into `b`, which on a shape's first use times the packed and equal z-chunk
  * grids (blocking once) and keeps the faster.  `a` is not changed; `b` is
  * overwritten (its ghost cells are not).  Then the same launch again for
- * about 25 ms of device time (at most 64 launches): after the GPU has idled
+ * about 25 ms of device time (at most 2048 launches): after the GPU has idled
  * its clock needs that long to settle (the first launches run up to 1.45x
- * slower), so a timed run that follows measures the settled state.  Blocks
- * the host once.  A no-op for jobs without a K-step launch.  No reference
- * counterpart (the reference has no per-shape state). */
+ * slower), so a timed run that follows measures the settled state.  2D jobs
+ * of K-step launches settle the same way (they have no per-shape choice).
+ * Blocks the host once.  A no-op for jobs without a K-step launch.  No
+ * reference counterpart (the reference has no per-shape state). */
 int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream);
 
 /* One resident grid instead of two (3D, no slab flags): for jobs whose two

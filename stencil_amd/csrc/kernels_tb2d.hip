@@ -229,15 +229,15 @@ int launch_tb1_r(const stencil_layout& l, const void* in, void* out, uint32_t it
 }
 
 // Strip variant (R <= V): strip2d.hpp.
-template <typename T, int ORDER, int R, int V, int RY, int NW>
+template <typename T, int ORDER, int R, int V, int RY, int NW, bool BF>
 __global__ void __launch_bounds__(64 * NW)
     tb2ds(const T* __restrict__ in, T* __restrict__ out, Geom g, int steps, int tiles_x, T avg) {
     __shared__ __attribute__((aligned(16))) strip2d::Lds<T, R, V, NW> L;
-    strip2d::region<T, ORDER, R, V, RY, NW>(in, out, g, steps, steps * R, int(blockIdx.x) % tiles_x,
-                                            int(blockIdx.x) / tiles_x, avg, L);
+    strip2d::region<T, ORDER, R, V, RY, NW, BF>(in, out, g, steps, steps * R, int(blockIdx.x) % tiles_x,
+                                                int(blockIdx.x) / tiles_x, avg, L);
 }
 
-template <typename T, int ORDER, int R, int V, int RY, int NW>
+template <typename T, int ORDER, int R, int V, int RY, int NW, bool BF = false>
 int launch_tbs(const stencil_layout& l, const void* in, void* out, int steps, hipStream_t s) {
     const Geom g = geom_of(l);
     if (g.nx <= 0 || g.ny <= 0 || steps <= 0) return STENCIL_OK;
@@ -246,7 +246,7 @@ int launch_tbs(const stencil_layout& l, const void* in, void* out, int steps, hi
     if (TX < 4 || TY < 4) return set_error(STENCIL_EINVAL, "tb2ds: %d steps of radius %d leave no tile", steps, R);
     const int64_t tx = (g.nx + TX - 1) / TX, ty = (g.ny + TY - 1) / TY;
     if (tx * ty > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "tb2ds: grid too large");
-    hipLaunchKernelGGL((tb2ds<T, ORDER, R, V, RY, NW>), dim3(unsigned(tx * ty)), dim3(64, NW), 0, s,
+    hipLaunchKernelGGL((tb2ds<T, ORDER, R, V, RY, NW, BF>), dim3(unsigned(tx * ty)), dim3(64, NW), 0, s,
                        static_cast<const T*>(in), static_cast<T*>(out), g, steps, int(tx), avg_weight<T>(l.prob));
     STENCIL_LAUNCH_CHECK();
     return STENCIL_OK;
@@ -268,14 +268,19 @@ int launch_shape(const stencil_layout& l, const void* in, void* out, int steps, 
         case 92216: return launch_tbs<T, ORDER, R, 2, 2, 16>(l, in, out, steps, s);
         case 94808: return launch_tbs<T, ORDER, R, 4, 8, 8>(l, in, out, steps, s);
         case 92608: return launch_tbs<T, ORDER, R, 2, 6, 8>(l, in, out, steps, s);
+        // the default shapes with branch-free ghost selects (strip2d::region BF; 9xxxx above branch per row)
+        case 192416: return launch_tbs<T, ORDER, R, 2, 4, 16, true>(l, in, out, steps, s);
+        case 192808: return launch_tbs<T, ORDER, R, 2, 8, 8, true>(l, in, out, steps, s);
         case 0:
             // default for r <= 2: 128 x 64 regions, 2 cells per lane (1024^2,
             // K = 8: fp64 559 vs 393 Gcell/s for the LDS kernel, fp32 709 vs
             // 520; tools/tb2d_ab.sh); fp64 as 16 waves x 4 rows (C1, K = 10: 694
             // vs 652 Gcell/s for 8 x 8 -- more waves hide the per-sweep
-            // barrier; tools/tb2ds_shape_ab.sh), fp32 as 8 x 8
-            if constexpr (sizeof(T) == 8) return launch_tbs<T, ORDER, R, 2, 4, 16>(l, in, out, steps, s);
-            return launch_tbs<T, ORDER, R, 2, 8, 8>(l, in, out, steps, s);
+            // barrier), fp32 as 8 x 8.  Branch-free ghost selects (round 4,
+            // tools/c1_ab.py, profiles/r04/r04d_c1_ab.txt): C1 fp64 762 vs 710,
+            // DMA order 799 vs 724, fp32 972 vs 856 Gcell/s, bitwise equal.
+            if constexpr (sizeof(T) == 8) return launch_tbs<T, ORDER, R, 2, 4, 16, true>(l, in, out, steps, s);
+            return launch_tbs<T, ORDER, R, 2, 8, 8, true>(l, in, out, steps, s);
         default: break;
         }
     }
@@ -339,7 +344,9 @@ int tb2d_steps(const stencil_layout& l, uint32_t iterations) {
     const stencil_problem& p = l.prob;
     const int base = tb2d_max_steps(p);
     const int cfg = tenv_int("STENCIL_TB2D_CFG", 0);
-    if (knob("STENCIL_TB2D_K", 0) != 0 || p.radius > 2 || (cfg != 0 && cfg != 92808 && cfg != 92416)) return base;  // 128 x 64 only
+    if (knob("STENCIL_TB2D_K", 0) != 0 || p.radius > 2 ||
+        (cfg != 0 && cfg % 100000 != 92808 && cfg % 100000 != 92416))
+        return base;  // 128 x 64 only
     const int slots = strip_slots();
     (void)hipGetLastError();
     if (slots <= 0) return base;

@@ -36,8 +36,10 @@ using Lds = T[2][NW][2][R][64 * V];  // [parity][wave][top, bottom][row][x]
 
 // One region of tile (bx, by): load tile + H-cell ring from `in`, `steps`
 // sweeps (steps * R <= H), store the tile to `out`.  Tiles are RW - 2H by
-// RH - 2H cells.
-template <typename T, int ORDER, int R, int V, int RY, int NW>
+// RH - 2H cells.  BF: every cell's update is computed and the ghost cells'
+// kept value chosen by a select (an empty asm pins the update, so the
+// compiler cannot sink it under an exec-mask branch per row).
+template <typename T, int ORDER, int R, int V, int RY, int NW, bool BF = false>
 __device__ __forceinline__ void region(const T* __restrict__ in, T* __restrict__ out, const Geom& g, int steps,
                                        int H, int bx, int by, T avg, Lds<T, R, V, NW>& L) {
     static_assert(R <= V, "one DPP shift reaches R cells");
@@ -128,6 +130,7 @@ __device__ __forceinline__ void region(const T* __restrict__ in, T* __restrict__
                     for (int d = 1; d <= R; ++d) sum += rowv(k + d)[j];
                     r = sum * avg;
                 }
+                if constexpr (BF) asm volatile("" : "+v"(r));
                 o[j] = (xin[j] && yin[k]) ? r : cv[j];  // ghost cells keep their value
             }
             b[k] = o;

@@ -121,19 +121,21 @@ def test_2d_radius_random(gpu, r, order):
 @pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma"), (3, "dma"), (4, "naive")])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("cfg", ["default", "8064", "4032", "16128", "12096", "8128", "92808", "92816", "92408",
-                                 "94808", "92416", "92216"])
+                                 "94808", "92416", "92216", "192808", "192416"])
 def test_2d_tile_resident_multistep(gpu, monkeypatch, k, r, order, dtype, cfg):
     """kernels_tb2d.hip: K sweeps per launch, every region shape of the LDS
-    kernel and of the register-strip kernel (cfg 9xxxx, r <= 2), ragged grids
-    spanning several tiles, iteration counts that leave a partial last launch."""
+    kernel and of the register-strip kernel (cfg 9xxxx, r <= 2; 19xxxx the
+    same strip shape with branch-free ghost selects), ragged grids spanning
+    several tiles, iteration counts that leave a partial last launch."""
     monkeypatch.setenv("STENCIL_TB2D_K", k)
     monkeypatch.setenv("STENCIL_TB2D_SINGLE", "0")  # the K-step launches even where one workgroup fits
     if cfg != "default":
         monkeypatch.setenv("STENCIL_TB2D_CFG", cfg)
-    strip = cfg.startswith("9") and r <= 2
-    rw = 64 * int(cfg[1]) if strip else 64
+    shape = cfg[1:] if len(cfg) == 6 else cfg
+    strip = shape.startswith("9") and r <= 2
+    rw = 64 * int(shape[1]) if strip else 64
     rh = {"default": 64, "8064": 64, "4032": 32, "16128": 128, "12096": 96, "8128": 128, "92808": 64, "92816": 128,
-          "92408": 32, "94808": 64, "92416": 64, "92216": 32}[cfg] if (strip or not cfg.startswith("9")) else 64
+          "92408": 32, "94808": 64, "92416": 64, "92216": 32}[shape] if (strip or not shape.startswith("9")) else 64
     if min(rw, rh) - 2 * min(int(k), 24 // r) * r < 4:
         pytest.skip("no tile left in this region for K sweeps")
     for nx, ny, it in ((301, 170, 11), (5, 3, 4), (64, 200, 9)):

@@ -14,6 +14,9 @@
 #   tier             tools/tier_pattern_bench 16 and 32 (the C2 decision gate)
 #   tierbench        the C2 bench through the two-tier launches (STENCIL_TK_TIER=1, debug library)
 #   ramp             tools/ramp_probe.py under a rocprofv3 kernel trace (per-launch durations by phase)
+#   sq:<cfg>         profiles/collect_sq.sh (SQ / LDS / TCC counter passes) of bench --config <cfg>
+#   nstrace          three separate NS bench processes, each under a kernel trace (per-launch durations per process)
+#   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
 TAG=$1; shift
@@ -44,10 +47,21 @@ for step in "$@"; do
     prof:*) c=${step#prof:}
             case "$c" in C5) a="--steps 8 --warmup 0";; *) a="--steps 100 --warmup 5";; esac
             bash profiles/collect.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/collect_$c.log" 2>&1 ;;
+    sq:*) c=${step#sq:}
+          case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 8 --warmup 0";; *) a="--steps 40 --warmup 4";; esac
+          PROG=bench.py bash profiles/collect_sq.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/sq_$c.log" 2>&1 ;;
     tier) timeout -k 10 120 tools/tier_pattern_bench 16 > "$O/tier16.txt" 2>&1 &&
           timeout -k 10 120 tools/tier_pattern_bench 32 > "$O/tier32.txt" 2>&1 ;;
     ramp) (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O/ramp" -o run -- \
              python3 "$R/tools/ramp_probe.py" > "$O/ramp.log" 2>&1) ;;
+    nstrace) for i in 1 2 3; do
+               (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/nstrace$i" \
+                 -o run -- python3 "$R/bench.py" --config NS --steps 40 --warmup 4 --no-cpu-baseline \
+                 > "$O/nstrace$i.json" 2>> "$O/bench.err") || exit 1
+             done ;;
+    c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 192416 > "$O/c1_ab.txt" 2>&1 &&
+          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 192416 >> "$O/c1_ab.txt" 2>&1 &&
+          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 192808 >> "$O/c1_ab.txt" 2>&1 ;;
     c1probe) timeout -k 10 120 python3 tools/c1_probe.py > "$O/c1_probe.txt" 2>&1 &&
              (cd /tmp && TMPDIR=/tmp timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d "$O/c1trace" \
                -o run -- python3 "$R/tools/c1_probe.py" --reps 10 > "$O/c1_probe_traced.txt" 2>&1) ;;

@@ -26,7 +26,7 @@ def short(name):
     table = (("tkstrip_7pt", "temporalk"), ("temporalk_7pt", "temporalk"), ("temporal2_7pt", "temporal2"),
              ("zmarch7", "zmarch"), ("sweep_direct", "direct"), ("box27_sep", "boxk"), ("box27_strip", "boxk"), ("boxk_27pt", "boxk"),
              ("copy_kernel", "copy_kernel"), ("fill_initial_kernel", "fill_initial_kernel"),
-             ("plane_sums", "plane_sums"))
+             ("plane_sums", "plane_sums"), ("tb2ds", "tb2ds"))
     for k, v in table:
         if k in name:
             return v
