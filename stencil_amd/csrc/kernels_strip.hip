@@ -328,8 +328,10 @@ __global__ void __launch_bounds__(64 * NW)
     uint32_t tier_pv = 0;  // the prefetched flag
     // the whole region inside the grid in x and y: intermediate stages need no
     // ghost-cell select on steps whose stage planes are all inside in z
-    const bool xy_inner = fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
-                          int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny;
+    // (fast == 2: every tile takes the fast path -- a timing experiment of the
+    // edge tiles' select cost, wrong ghost cells; STENCIL_TK_FAST=2, debug library)
+    const bool xy_inner = fast == 2 || (fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
+                                        int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny);
     const int ld_lo = halo_lo ? -K : -1;
     const int ld_hi = halo_hi ? nz + K - 1 : nz;
     const int zfirst = za - K > ld_lo ? za - K : ld_lo;

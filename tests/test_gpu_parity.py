@@ -491,6 +491,37 @@ def test_temporalk_signed_zero_field(gpu, shape, steps, dtype):
     assert same_bits(np.ascontiguousarray(got), np.ascontiguousarray(a))
 
 
+@pytest.mark.parametrize("r,order", [(1, "naive"), (1, "dma"), (2, "naive"), (2, "dma")])
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("cfg", ["default", "92416", "92808"])
+def test_2d_strip_signed_zero_field(gpu, monkeypatch, r, order, dtype, cfg):
+    """The 2D strip region folds the reference's leading `0 +` into
+    fma(sum, avg, +0) (strip2d.hpp fma0): a block of -0.0 cells with -0.0
+    ghosts beside it (where 0 + -0 = +0 matters) and mixed-sign data, through
+    AUTO's K-step launches, bit for bit the oracle's plain sweeps."""
+    import torch
+    if cfg != "default":
+        monkeypatch.setenv("STENCIL_TB2D_CFG", cfg)
+    nx, ny, it = 301, 170, 23
+    e = engine(gpu, 2, dtype, "star", r, order, "auto", nx, ny, 1)
+    e.reset("random", 13)
+    full = e.with_ghosts(e.a)
+    full[:, : nx // 3] = -0.0          # ghost column and ghost rows included
+    full[60:90, :] *= -1.0
+    full[100:110, 200:] = 0.0
+    torch.cuda.synchronize()
+    start = full.cpu().numpy().copy()
+    e.with_ghosts(e.b).copy_(full)
+    p = ob.problem(2, dtype, "star", r, order, nx, ny)
+    a, b = start.copy(), start.copy()
+    for _ in range(it):
+        ob.sweep(p, a, b, 0, ny)
+        a, b = b, a
+    assert (np.signbit(a) & (a == 0)).any() and (~np.signbit(a) & (a == 0)).any()
+    fin, _ = e.iterate(it)
+    assert same_bits(e.to_numpy(fin), a)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("zchunk", ["0", "3", "8"])
 def test_box_single_sweeps(gpu, monkeypatch, dtype, zchunk):

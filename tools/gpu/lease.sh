@@ -16,6 +16,7 @@
 #   ramp             tools/ramp_probe.py under a rocprofv3 kernel trace (per-launch durations by phase)
 #   sq:<cfg>         profiles/collect_sq.sh (SQ / LDS / TCC counter passes) of bench --config <cfg>
 #   nstrace          three separate NS bench processes, each under a kernel trace (per-launch durations per process)
+#   fastab           tools/ab.py at 512^3: the interior fast path as shipped vs on every tile (timing only) vs off
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -59,9 +60,12 @@ for step in "$@"; do
                  -o run -- python3 "$R/bench.py" --config NS --steps 40 --warmup 4 --no-cpu-baseline \
                  > "$O/nstrace$i.json" 2>> "$O/bench.err") || exit 1
              done ;;
-    c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 192416 > "$O/c1_ab.txt" 2>&1 &&
-          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 192416 >> "$O/c1_ab.txt" 2>&1 &&
-          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 192808 >> "$O/c1_ab.txt" 2>&1 ;;
+    fastab) timeout -k 10 180 python3 tools/ab.py --grid 512 512 512 --steps 4 --reps 9 --launches 10 \
+              --variant STENCIL_TK_FAST=1 --variant STENCIL_TK_FAST=2,NOCHECK=1 --variant STENCIL_TK_FAST=0 \
+              > "$O/fast_ab.txt" 2>&1 ;;
+    c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
+          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 92416 >> "$O/c1_ab.txt" 2>&1 &&
+          timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 92808 >> "$O/c1_ab.txt" 2>&1 ;;
     c1probe) timeout -k 10 120 python3 tools/c1_probe.py > "$O/c1_probe.txt" 2>&1 &&
              (cd /tmp && TMPDIR=/tmp timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d "$O/c1trace" \
                -o run -- python3 "$R/tools/c1_probe.py" --reps 10 > "$O/c1_probe_traced.txt" 2>&1) ;;
