@@ -17,6 +17,9 @@
 #   sq:<cfg>         profiles/collect_sq.sh (SQ / LDS / TCC counter passes) of bench --config <cfg>
 #   nstrace          three separate NS bench processes, each under a kernel trace (per-launch durations per process)
 #   fastab           tools/ab.py at 512^3: the interior fast path as shipped vs on every tile (timing only) vs off
+#   libab:<t1,t2..>  tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
+#                    alternating the variants, 3 rounds over C2 / 2048^2 x 512 / NS / fp32 4096^2 x 256
+#   libabbox:<t,..>  the same over box shapes: C5 2048^3 / 2048^2 x 256 / 512^3 fp64
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -63,6 +66,27 @@ for step in "$@"; do
     fastab) timeout -k 10 180 python3 tools/ab.py --grid 512 512 512 --steps 4 --reps 9 --launches 10 \
               --variant STENCIL_TK_FAST=1 --variant STENCIL_TK_FAST=2,NOCHECK=1 --variant STENCIL_TK_FAST=0 \
               > "$O/fast_ab.txt" 2>&1 ;;
+    libab:*) IFS=',' read -r -a tags <<< "${step#libab:}"
+             for rep in 1 2 3; do
+               for shp in "star fp64 512 512 512 1000 2" "star fp64 2048 2048 512 200 2" "star fp64 2048 2048 2048 40 2" \
+                          "star fp32 4096 4096 256 200 2"; do
+                 for t in "${tags[@]}"; do
+                   # shellcheck disable=SC2086
+                   timeout -k 10 120 python3 tools/time_lib.py "build/variants/lib_$t.so" $shp >> "$O/lib_ab.txt" 2>> "$O/lib_ab.err" \
+                     || exit 1
+                 done
+               done
+             done ;;
+    libabbox:*) IFS=',' read -r -a tags <<< "${step#libabbox:}"
+             for rep in 1 2 3; do
+               for shp in "box fp64 2048 2048 2048 16 2" "box fp64 2048 2048 256 40 2" "box fp64 512 512 512 200 2"; do
+                 for t in "${tags[@]}"; do
+                   # shellcheck disable=SC2086
+                   timeout -k 10 120 python3 tools/time_lib.py "build/variants/lib_$t.so" $shp >> "$O/lib_ab_box.txt" \
+                     2>> "$O/lib_ab.err" || exit 1
+                 done
+               done
+             done ;;
     c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 92416 >> "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 92808 >> "$O/c1_ab.txt" 2>&1 ;;
