@@ -80,6 +80,13 @@ const Rccl& rccl() {
             return set_error(STENCIL_EHIP, "%s failed: %s", #expr, rccl().GetErrorString(e_));        \
     } while (0)
 
+// one lane spins `ticks` of s_memrealtime (100 MHz): HipDev::debug_delay
+__global__ void __launch_bounds__(64) delay_kernel(uint64_t ticks) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
+}
+
 }  // namespace
 
 // ---- the HIP + RCCL backend of slab_core.hpp ------------------------------
@@ -108,6 +115,20 @@ struct HipDev {
         return 1;
     }
     static bool signal_enabled() { return api_knob("STENCIL_SLAB_SIGNAL", 1) != 0; }
+    // STENCIL_SLAB_NO_PULL_WAIT=1 (debug library, the test that shows the
+    // delay below exposing the race): drop the rolling exchange's wait
+    static bool pull_wait_enabled() { return knob("STENCIL_SLAB_NO_PULL_WAIT", 0) == 0; }
+    // STENCIL_SLAB_COPY_DELAY_US (debug library, tests): a one-lane spin of
+    // that many microseconds queued before slab 0 pulls its neighbours' faces
+    // (the others run on), so that a missing stream dependency of the copy
+    // exchange shows every time
+    static int debug_delay(Stream s, int slab) {
+        const int us = knob("STENCIL_SLAB_COPY_DELAY_US", 0);
+        if (us <= 0 || slab != 0) return STENCIL_OK;
+        hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, uint64_t(us) * 100);
+        STENCIL_HIP_CHECK(hipGetLastError());
+        return STENCIL_OK;
+    }
     static int free_bytes(int64_t* out) {
         size_t fr = 0, tot = 0;
         STENCIL_HIP_CHECK(hipMemGetInfo(&fr, &tot));

@@ -205,6 +205,7 @@ int exchange(Job<Dev>& j, int pos) {
         void* g = grid_at(j, s, pos);
         const size_t bytes = size_t(d) * plane_bytes(s);
         const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+        SLAB_TRY(Dev::debug_delay(s.sa, i));  // tests: slab 0's pulls slow (a no-op unless asked for)
         if (lo >= 0) {
             Slab<Dev>& t = j.s[size_t(lo)];
             SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
@@ -216,6 +217,25 @@ int exchange(Job<Dev>& j, int pos) {
             SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
             SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, s.n), s.device, plane_ptr(t, grid_at(j, t, pos), 0), t.device, bytes,
                                     s.sa));
+        }
+    }
+    if (j.margin && Dev::pull_wait_enabled()) {
+        // Rolling slabs: a slab's next pass writes its new grid over the
+        // planes its neighbours are still pulling faces from (the grid moves
+        // by the shift every round), so every slab waits for its neighbours'
+        // pulls first.  Two-grid jobs need no such wait: the next round
+        // writes the other grid, and the round after waits on this one.
+        // (RCCL exchanges are ordered by each slab's own stream.)
+        for (Slab<Dev>& s : j.s) {
+            SLAB_TRY(Dev::set_device(s.device));
+            SLAB_TRY(Dev::event_record(s.ev_join, s.sa));
+        }
+        for (int i = 0; i < n; ++i) {
+            Slab<Dev>& s = j.s[size_t(i)];
+            SLAB_TRY(Dev::set_device(s.device));
+            const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+            if (lo >= 0 && lo != i) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(lo)].ev_join));
+            if (hi >= 0 && hi != i && hi != lo) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(hi)].ev_join));
         }
     }
     return STENCIL_OK;

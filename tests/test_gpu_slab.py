@@ -364,6 +364,48 @@ def test_signalled_rounds_over_rccl(gpu, monkeypatch, shape):
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
+def _rolling_copy_job(gpu, dtype, shape, nslabs, margin_extra=1):
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz, it = 70, 45, 23 * nslabs + 1, 11
+    ref = JacobiEngine(StencilSpec(dims=3, dtype=dtype, shape=shape, kernel="direct"), nx, ny, nz, device=gpu)
+    ref.reset("random", 3)
+    fin, _ = ref.iterate(it)
+    want = ref.to_numpy(fin)
+    k = JacobiEngine(spec, nx, ny, nz, device=gpu, allocate=False).fuse_steps
+    job = SlabJob(spec, nx, ny, nz, [gpu] * nslabs, exchange="copy", rolling=True, margin=k + margin_extra)
+    try:
+        job.fill_initial("random", 3)
+        job.run(it)
+        got = job.download()
+    finally:
+        job.close()
+    return got, want
+
+
+@pytest.mark.parametrize("dtype,shape", [("fp64", "star"), ("fp32", "box")])
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_rolling_slabs_slow_face_pulls(gpu, monkeypatch, dtype, shape, nslabs):
+    """A rolling slab's next pass writes its new grid over the planes its
+    neighbours pull faces from, so the copy exchange holds every slab until
+    its neighbours' pulls are done (slab_core.hpp exchange).  A 3 ms spin
+    before slab 0's pulls (STENCIL_SLAB_COPY_DELAY_US, debug library; its
+    neighbour runs on) makes a missing dependency show every time: round 4's
+    intermittent mismatch of
+    test_rolling_slabs_equal_one_grid[3-fp32-box] was this race."""
+    monkeypatch.setenv("STENCIL_SLAB_COPY_DELAY_US", "3000")
+    got, want = _rolling_copy_job(gpu, dtype, shape, nslabs)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+def test_rolling_slabs_slow_face_pulls_need_the_wait(gpu, monkeypatch):
+    """The test above has teeth: with the wait dropped (debug knob) the slow
+    pulls read planes the neighbour's next pass has already overwritten."""
+    monkeypatch.setenv("STENCIL_SLAB_COPY_DELAY_US", "3000")
+    monkeypatch.setenv("STENCIL_SLAB_NO_PULL_WAIT", "1")
+    got, want = _rolling_copy_job(gpu, "fp64", "star", 3)
+    assert not np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
 @pytest.mark.parametrize("dtype,shape", [("fp64", "star"), ("fp32", "box")])
 @pytest.mark.parametrize("nslabs", [1, 2, 3])
 def test_rolling_slabs_equal_one_grid(gpu, dtype, shape, nslabs):
