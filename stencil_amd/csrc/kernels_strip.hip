@@ -52,13 +52,6 @@
 #ifndef TK_FAST_PATH
 #define TK_FAST_PATH 1
 #endif
-// TK_BUFST: one-cell-per-lane shapes store through a buffer resource (the
-// output plane's base in SGPRs, the row's 32-bit byte offset as voffset);
-// lanes and rows outside the tile get an out-of-range offset, which the
-// hardware drops -- no exec-mask branch and no 64-bit address per store
-#ifndef TK_BUFST
-#define TK_BUFST 0
-#endif
 
 namespace stencil {
 namespace {
@@ -67,24 +60,6 @@ template <typename T, int V>
 struct VecS {
     typedef T type __attribute__((ext_vector_type(V)));
 };
-
-// buffer stores (TK_BUFST): gfx9 raw-buffer word 3 (as composable_kernel's
-// CK_BUFFER_RESOURCE_3RD_DWORD), a range of 2^32 - 4096 bytes from the plane's
-// biased base (the host keeps every row offset below it), an offset past it
-// for lanes that must not store, and the nt cache policy of the global stores
-typedef unsigned int BufU32x2 __attribute__((ext_vector_type(2)));
-constexpr unsigned kBufRecords = 0xFFFFF000u;
-constexpr unsigned kBufOob = 0xFFFFF800u;
-constexpr int kBufWord3 = 0x00020000;
-constexpr int kBufNt = 2;
-
-template <typename VV>
-__device__ __forceinline__ void buf_store64(const VV& v, char* base, uint32_t voffset) {
-    if constexpr (sizeof(VV) == 8) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, short(0), int(kBufRecords), kBufWord3);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(BufU32x2, v), r, voffset, 0, kBufNt);
-    }
-}
 
 __device__ __forceinline__ float sfma0(float s, float a) { return __builtin_fmaf(s, a, 0.0f); }
 __device__ __forceinline__ double sfma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
@@ -331,16 +306,6 @@ __global__ void __launch_bounds__(64 * NW)
         xin[j] = x + j >= 0 && x + j < g.nx;
         xst[j] = x + j < g.nx;
     }
-    // TK_BUFST: the row part of st[] as scalar flags (the wave index is
-    // uniform), the lane part as one offset mask OR-ed into the row offset
-    bool rowst[RY];
-    {
-        const int wu = __builtin_amdgcn_readfirstlane(w);
-        const int64_t yu = int64_t(by) * TY - K + int64_t(wu) * RY;
-#pragma unroll
-        for (int k = 0; k < RY; ++k) rowst[k] = wu * RY + k >= K && wu * RY + k < RH - K && yu + k < g.ny;
-    }
-    const uint32_t lane_oob = (lane >= XR && lane < 64 - XR && xst[0]) ? 0u : kBufOob;
     // TIER producer: the slot cells this lane stores per row -- its output
     // tile's, and the region's ghost cells (x in {-1, nx} or y in {-1, ny}:
     // ghost cells never change, and the consumers' regions read them from the
@@ -489,7 +454,6 @@ __global__ void __launch_bounds__(64 * NW)
         const int zo = p - K;  // t_K(p-K) -> HBM
         const bool do_store = DIAG != 3 && zo >= za && zo < zb;
         char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
-        constexpr bool kBufSt = TK_BUFST && V == 1 && sizeof(T) == 8 && !PROD && DIAG != 3;  // fp64, one cell per lane
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             VT prev{};  // this row's result of the previous stage
@@ -544,14 +508,6 @@ __global__ void __launch_bounds__(64 * NW)
                 if (do_store && ((st[k] && xin[0]) || (yghost && xspan) || (xghost && yspan)))
                     sc1_store<VT>(const_cast<char*>(slots) + int64_t(zo & tier.rmask) * plane * int64_t(sizeof(T)) +
                                       off[k], prev);
-                continue;
-            }
-            if constexpr (kBufSt) {
-                if (do_store && rowst[k]) {  // uniform condition
-                    uint32_t m = lane_oob;
-                    asm volatile("" : "+v"(m));  // opaque per use: the 7 row offsets are not hoisted as 7 more VGPRs
-                    buf_store64(prev, obase, off[k] | m);
-                }
                 continue;
             }
             if (do_store && st[k]) {
@@ -669,8 +625,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
     if (nz <= 0 || g.nx <= 0 || g.ny <= 0) return STENCIL_OK;
-    // row offsets are 32-bit byte offsets from a plane's base, below the buffer range of the stores (kBufRecords)
-    if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= int64_t(kBufRecords) || g.nz + 2 * K >= (int64_t(1) << 30))
+    if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
     auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP, HL>;

@@ -17,7 +17,7 @@
 #   sq:<cfg>         profiles/collect_sq.sh (SQ / LDS / TCC counter passes) of bench --config <cfg>
 #   nstrace          three separate NS bench processes, each under a kernel trace (per-launch durations per process)
 #   fastab           tools/ab.py at 512^3: the interior fast path as shipped vs on every tile (timing only) vs off
-#   libab:<t1,t2..>  tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
+#   libab:<t1,t2..>  (LIBAB_FP32_ONLY=1: fp32 shapes only) tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
 #                    alternating the variants, 3 rounds over C2 / 2048^2 x 512 / NS / fp32 4096^2 x 256
 #   libabbox:<t,..>  the same over box shapes: C5 2048^3 / 2048^2 x 256 / 512^3 fp64
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
@@ -68,8 +68,10 @@ for step in "$@"; do
               > "$O/fast_ab.txt" 2>&1 ;;
     libab:*) IFS=',' read -r -a tags <<< "${step#libab:}"
              for rep in 1 2 3; do
-               for shp in "star fp64 512 512 512 1000 2" "star fp64 2048 2048 512 200 2" "star fp64 2048 2048 2048 40 2" \
-                          "star fp32 4096 4096 256 200 2"; do
+               shapes=("star fp64 512 512 512 1000 2" "star fp64 2048 2048 512 200 2" "star fp64 2048 2048 2048 40 2"
+                       "star fp32 4096 4096 256 200 2")
+               [ -n "${LIBAB_FP32_ONLY:-}" ] && shapes=("star fp32 4096 4096 256 200 2" "star fp32 2048 2048 512 200 2")
+               for shp in "${shapes[@]}"; do
                  for t in "${tags[@]}"; do
                    # shellcheck disable=SC2086
                    timeout -k 10 120 python3 tools/time_lib.py "build/variants/lib_$t.so" $shp >> "$O/lib_ab.txt" 2>> "$O/lib_ab.err" \
