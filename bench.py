@@ -126,6 +126,10 @@ def parse(argv=None):
                          "halos are its own faces, by device copies / RCCL send-recv to itself)")
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal without a launcher: every slab on GPU 0 (needs --exchange copy)")
+    ap.add_argument("--rank-of", type=int, default=0, metavar="N",
+                    help="with --exchange loopback | nccl-self: rehearse ONE interior rank of the N-GPU job (its "
+                         "slab of the config's global grid, two grids or rolling as the N-GPU plan says, periodic "
+                         "halos) on one GPU -- e.g. --config NS4096 --rank-of 2")
     ap.add_argument("--rolling", choices=["auto", "on", "off"], default="auto",
                     help="slabs: ONE grid + a rolling margin (on), two grids (off), or whatever fits (auto)")
     ap.add_argument("--init", choices=["reference", "random"], default="reference",
@@ -147,6 +151,9 @@ def parse(argv=None):
                          "unset them or pass --allow-debug-library")
     if args.no_signal:
         os.environ["STENCIL_SLAB_SIGNAL"] = "0"  # an API knob: read at slab creation
+    if args.rank_of and (args.rank_of < 2 or args.gpus != 1 or args.exchange not in ("loopback", "nccl-self")):
+        raise SystemExit("--rank-of N (N >= 2) rehearses one rank of an N-GPU job on ONE GPU: it needs --gpus 1 and "
+                         "--exchange loopback or nccl-self")
     return args
 
 
@@ -645,7 +652,15 @@ def main_slab_job(args):
     free = torch.cuda.mem_get_info(0)[0]
     shared = len(set(devices)) < len(devices)
     # slabs sharing GPU 0 share its memory too
-    plan = slab_plan(args.config, n_gpus, free // (n_gpus if shared else 1), args.n, args.rolling)
+    plan = rank_plan = None
+    if args.rank_of:
+        # one interior rank of the N-GPU job: the N-way plan (per-GPU memory =
+        # this GPU's), then that rank's slab alone, its halos its own faces
+        rank_plan = slab_plan(args.config, args.rank_of, free, args.n, args.rolling)
+        gnx, gny, gz = rank_plan["grid"]
+        plan = dict(rank_plan, grid=(gnx, gny, rank_plan["planes_per_slab"]))
+    else:
+        plan = slab_plan(args.config, n_gpus, free // (n_gpus if shared else 1), args.n, args.rolling)
     spec = _slab_spec(args, pre)
     gnx, gny, gnz = plan["grid"]
     job = SlabJob(spec, gnx, gny, gnz, devices, exchange=exchange, periodic=loop, rolling=plan["rolling"], margin=0)
@@ -673,9 +688,13 @@ def main_slab_job(args):
     form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
         "boundary + interior launches"
     if loop:
-        parallelism = ("1 GPU rehearsing an interior rank: one periodic slab whose halos are its own faces, " +
+        parallelism = ("1 GPU rehearsing an interior rank" +
+                       (f" of the {args.rank_of}-GPU job (its {gnz}-plane slab of the "
+                        f"{'x'.join(str(v) for v in rank_plan['grid'])} grid)" if args.rank_of else "") +
+                       ": one periodic slab whose halos are its own faces, " +
                        ("device copies" if exchange == "copy" else "RCCL send/recv to itself") +
-                       " (C-ABI slab job)")
+                       " (C-ABI slab job)" +
+                       (f"; ONE grid + a rolling margin of {roll['margin']} planes" if roll["margin"] else ""))
     else:
         where = "GPU 0 shared by every slab (rehearsal)" if args.share_device else f"{n_gpus} GPUs"
         parallelism = (f"z-slab x{n_gpus}, ONE process driving {where} through the C-ABI slab job (stencil_slab_*), " +
@@ -685,10 +704,12 @@ def main_slab_job(args):
            float(kt["cells_per_launch"]), k, kt["launches"], parallelism, rounds=form,
            launch_timing=f"hipEvents around slab 0's {form} of extra rounds after the timed region",
            workload_key=(f"3d7pt_fp64_{args.n}cube_per_gpu_slab_x{n_gpus}" if args.config == "C2" else
-                         f"{args.config}_slab_{gnz // n_gpus}_x{n_gpus}") + ("_loop" if loop else ""),
+                         f"{args.config}_slab_{gnz // n_gpus}_x{args.rank_of or n_gpus}") + ("_loop" if loop else ""),
            local=0, check=check if n_gpus > 1 else None, cpu=False,
            kernels_per_launch=float(max(1, roll["launches_per_pass"])) if roll["margin"] else 1.0,
-           extra_config={"slab_plan": {k2: v for k2, v in plan.items() if k2 != "grid"}})
+           extra_config=dict({"slab_plan": {k2: v for k2, v in plan.items() if k2 != "grid"}},
+                             **({"rank_of": args.rank_of, "global_grid": list(rank_plan["grid"])} if args.rank_of
+                                else {})))
 
 
 def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,

@@ -112,3 +112,22 @@ def test_old_python_driver_flags_are_gone():
         with pytest.raises(SystemExit):
             bench.parse(["--gpus", "2", flag] + (["python"] if flag == "--driver" else []))
     assert not os.path.exists(os.path.join(ROOT, "stencil_amd", "slab.py"))
+
+
+@pytest.mark.parametrize("argv,reason", [
+    (["--rank-of", "2"], "needs --gpus 1 and --exchange loopback or nccl-self"),
+    (["--rank-of", "1", "--exchange", "loopback"], "N >= 2"),
+    (["--rank-of", "4", "--gpus", "2", "--exchange", "loopback"], "needs --gpus 1"),
+])
+def test_rank_of_needs_a_one_gpu_loopback_rehearsal(argv, reason):
+    with pytest.raises(SystemExit, match=reason):
+        bench.parse(["--config", "NS4096"] + argv)
+
+
+def test_rank_of_parses_for_the_north_star():
+    """`--config NS4096 --rank-of 2 --exchange loopback`: one rank's slab of the
+    2-GPU job (4096^2 x 2048 planes, rolling as that plan says) on ONE GPU."""
+    a = bench.parse(["--config", "NS4096", "--rank-of", "2", "--exchange", "loopback"])
+    assert a.rank_of == 2 and a.gpus == 1
+    plan = bench.slab_plan("NS4096", a.rank_of, BOX_FREE)
+    assert plan["planes_per_slab"] == 2048 and plan["rolling"]

@@ -20,6 +20,7 @@
 #   libab:<t1,t2..>  (LIBAB_FP32_ONLY=1: fp32 shapes only) tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
 #                    alternating the variants, 3 rounds over C2 / 2048^2 x 512 / NS / fp32 4096^2 x 256
 #   libabbox:<t,..>  the same over box shapes: C5 2048^3 / 2048^2 x 256 / 512^3 fp64
+#   rankof:<cfg>:<N> bench.py --config <cfg> --rank-of N --exchange loopback: one interior rank of the N-GPU job
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -89,6 +90,10 @@ for step in "$@"; do
                  done
                done
              done ;;
+    rankof:*) r=${step#rankof:}; c=${r%%:*}; nr=${r##*:}
+             case "$c" in C5) a="--steps 16 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+             timeout -k 10 400 python3 bench.py --config "$c" --rank-of "$nr" --exchange loopback $a --no-cpu-baseline \
+               > "$O/bench_${c}_rank_of_$nr.json" 2>> "$O/bench.err" ;;
     c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 92416 >> "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 92808 >> "$O/c1_ab.txt" 2>&1 ;;
