@@ -331,6 +331,9 @@ int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     stencil_layout l{};
     l.prob = p;
     l.row = (origin_x + p.nx + r + align - 1) / align * align;
+    // STENCIL_ROW_PAD (debug library, experiments): extra elements per row, in
+    // whole 128-B units (the row pitch's effect on wide planes)
+    l.row += (std::max(0, knob("STENCIL_ROW_PAD", 0)) + align - 1) / align * align;
     l.rows = p.ny + 2 * r;
     l.plane = l.row * l.rows;
     l.zghost = p.dims == 3 ? std::max<int64_t>(r, p.halo) : 0;

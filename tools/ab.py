@@ -72,7 +72,10 @@ def main():
             print(f"variant {v}: bitwise equal to {refs[k][0] or 'default'}: {same}", flush=True)
             if not same:
                 raise SystemExit(1)
+        del out  # only the first output of each step count is kept (wide grids: one interior is 64 GB)
+        torch.cuda.empty_cache()
     del refs
+    torch.cuda.empty_cache()
     for _ in range(args.reps):
         for vi, v in enumerate(variants):
             setenv(v)

@@ -20,7 +20,10 @@
 #   libab:<t1,t2..>  (LIBAB_FP32_ONLY=1: fp32 shapes only) tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
 #                    alternating the variants, 3 rounds over C2 / 2048^2 x 512 / NS / fp32 4096^2 x 256
 #   libabbox:<t,..>  the same over box shapes: C5 2048^3 / 2048^2 x 256 / 512^3 fp64
-#   rankof:<cfg>:<N> bench.py --config <cfg> --rank-of N --exchange loopback: one interior rank of the N-GPU job
+#   rankof:<cfg>:<N>[:nosig] bench.py --config <cfg> --rank-of N --exchange loopback: one interior rank of the N-GPU job
+#   plain:<star|box>:<dt>:nx:ny:nz:sweeps  tools/time_lib.py on the product library (one grid, AUTO)
+#   zcab             tools/ab.py on 4096^2 x 512 fp64: z-chunk lengths (STENCIL_TK_ZCHUNK) of the wide-plane strip launch
+#   padscan:nx:ny:nz:sweeps  tools/time_lib.py (debug library) over STENCIL_ROW_PAD = 0 .. 512 elements
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -90,10 +93,24 @@ for step in "$@"; do
                  done
                done
              done ;;
-    rankof:*) r=${step#rankof:}; c=${r%%:*}; nr=${r##*:}
+    rankof:*) IFS=':' read -r c nr ns <<< "${step#rankof:}"
              case "$c" in C5) a="--steps 16 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+             [ "$ns" = nosig ] && a="$a --no-signal"
              timeout -k 10 400 python3 bench.py --config "$c" --rank-of "$nr" --exchange loopback $a --no-cpu-baseline \
-               > "$O/bench_${c}_rank_of_$nr.json" 2>> "$O/bench.err" ;;
+               > "$O/bench_${c}_rank_of_$nr${ns:+_$ns}.json" 2>> "$O/bench.err" ;;
+    plain:*) IFS=':' read -r shp dt nx ny nz sw <<< "${step#plain:}"   # the single-grid kernel rate of one shape
+             timeout -k 10 300 python3 tools/time_lib.py stencil_amd/libstencil_hip.so "$shp" "$dt" "$nx" "$ny" "$nz" "$sw" 3 \
+               >> "$O/plain.txt" 2>> "$O/bench.err" ;;
+    zcab) STENCIL_TK_VERBOSE=1 timeout -k 10 300 python3 tools/ab.py --grid 4096 4096 512 --steps 4 --reps 5 --launches 3 \
+              --variant STENCIL_TK_ZCHUNK=0 --variant STENCIL_TK_ZCHUNK=256 --variant STENCIL_TK_ZCHUNK=128 \
+              --variant STENCIL_TK_ZCHUNK=64 --variant STENCIL_TK_ZCHUNK=32 > "$O/zc_ab.txt" 2>&1 ;;
+    padscan:*) IFS=':' read -r nx ny nz sw <<< "${step#padscan:}"
+             for rep in 1 2; do
+               for pad in 0 16 32 64 128 256 512 1024; do
+                 STENCIL_ROW_PAD=$pad timeout -k 10 200 python3 tools/time_lib.py stencil_amd/libstencil_hip_debug.so star fp64 \
+                   "$nx" "$ny" "$nz" "$sw" 2 | sed "s/^/pad $pad: /" >> "$O/padscan.txt" 2>> "$O/bench.err" || exit 1
+               done
+             done ;;
     c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 92416 >> "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 92808 >> "$O/c1_ab.txt" 2>&1 ;;
