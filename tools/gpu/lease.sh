@@ -23,7 +23,7 @@
 #   rankof:<cfg>:<N>[:nosig] bench.py --config <cfg> --rank-of N --exchange loopback: one interior rank of the N-GPU job
 #   plain:<star|box>:<dt>:nx:ny:nz:sweeps  tools/time_lib.py on the product library (one grid, AUTO)
 #   zcab             tools/ab.py on 4096^2 x 512 fp64: z-chunk lengths (STENCIL_TK_ZCHUNK) of the wide-plane strip launch
-#   padscan:nx:ny:nz:sweeps  tools/time_lib.py (debug library) over STENCIL_ROW_PAD = 0 .. 512 elements
+#   padscan:nx:ny:nz:sweeps[:dtype[:pad,pad..]]  tools/time_lib.py (debug library) over STENCIL_ROW_PAD values
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -104,10 +104,11 @@ for step in "$@"; do
     zcab) STENCIL_TK_VERBOSE=1 timeout -k 10 300 python3 tools/ab.py --grid 4096 4096 512 --steps 4 --reps 5 --launches 3 \
               --variant STENCIL_TK_ZCHUNK=0 --variant STENCIL_TK_ZCHUNK=256 --variant STENCIL_TK_ZCHUNK=128 \
               --variant STENCIL_TK_ZCHUNK=64 --variant STENCIL_TK_ZCHUNK=32 > "$O/zc_ab.txt" 2>&1 ;;
-    padscan:*) IFS=':' read -r nx ny nz sw <<< "${step#padscan:}"
+    padscan:*) IFS=':' read -r nx ny nz sw dt pads <<< "${step#padscan:}"
+             dt=${dt:-fp64}; pads=${pads:-0,16,32,64,128,256,512,1024}
              for rep in 1 2; do
-               for pad in 0 16 32 64 128 256 512 1024; do
-                 STENCIL_ROW_PAD=$pad timeout -k 10 200 python3 tools/time_lib.py stencil_amd/libstencil_hip_debug.so star fp64 \
+               for pad in ${pads//,/ }; do
+                 STENCIL_ROW_PAD=$pad timeout -k 10 200 python3 tools/time_lib.py stencil_amd/libstencil_hip_debug.so star "$dt" \
                    "$nx" "$ny" "$nz" "$sw" 2 | sed "s/^/pad $pad: /" >> "$O/padscan.txt" 2>> "$O/bench.err" || exit 1
                done
              done ;;
