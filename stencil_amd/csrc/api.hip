@@ -321,6 +321,8 @@ const char* stencil_strerror(int code) {
 const char* stencil_last_error_message(void) { return g_last_msg; }
 int stencil_last_error(void) { return g_last_code; }
 
+constexpr int64_t kPitchPeriod = 32768, kPitchNear = 256;  // bytes (stencil_layout_init's pitch rule)
+
 int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     if (int rc = check_problem(prob)) return rc;
     if (!out) return set_error(STENCIL_EINVAL, "null layout");
@@ -331,8 +333,21 @@ int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     stencil_layout l{};
     l.prob = p;
     l.row = (origin_x + p.nx + r + align - 1) / align * align;
+    // Row pitches of 32 KiB or more that sit at most 256 B above a multiple of
+    // 32 KiB run the K-step kernels 20-30 % slower: 4096-wide fp64 planes
+    // (33024 B) 1055 Gcell/s against 1360 with 128 B more, 8192-wide fp32
+    // (32896 B) 1918 against 2388 with 128 B more, 8192-wide fp64 (65792 B)
+    // 1019 against 1260 with 2 KiB more (128 B more: 997).  Such rows get 128 B
+    // below 64 KiB, 2 KiB above.  Every other measured pitch ran best unpadded
+    // (512, 2048, 3072 and 4000 wide fp64, 4096 wide fp32): DESIGN.md §9.1i,
+    // profiles/r04/r04q_*, r04r_*, r04s_*.
+    {
+        const int64_t pitch = l.row * int64_t(elem_size(p));
+        if (pitch >= kPitchPeriod && pitch % kPitchPeriod <= kPitchNear)
+            l.row += (pitch < 2 * kPitchPeriod ? 128 : 2048) / int64_t(elem_size(p));
+    }
     // STENCIL_ROW_PAD (debug library, experiments): extra elements per row, in
-    // whole 128-B units (the row pitch's effect on wide planes)
+    // whole 128-B units (the row-pitch scans)
     l.row += (std::max(0, knob("STENCIL_ROW_PAD", 0)) + align - 1) / align * align;
     l.rows = p.ny + 2 * r;
     l.plane = l.row * l.rows;

@@ -200,6 +200,8 @@ struct FakeDev {
         stencil_layout l{};
         l.prob = *p;
         l.row = (origin_x + p->nx + r + align - 1) / align * align;
+        if (32768 <= l.row * es && (l.row * es) % 32768 <= 256)  // api.hip's pitch rule
+            l.row += (l.row * es < 65536 ? 128 : 2048) / es;
         l.rows = p->ny + 2 * r;
         l.plane = l.row * l.rows;
         l.zghost = std::max<int64_t>(r, p->halo);

@@ -364,6 +364,27 @@ def test_signalled_rounds_over_rccl(gpu, monkeypatch, shape):
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
+@pytest.mark.parametrize("rolling", [False, True])
+def test_slabs_on_a_padded_row_pitch(gpu, rolling):
+    """4096-wide fp64 planes take a padded row pitch (stencil_layout_init):
+    whole-plane halo copies between slabs and rolling passes on that layout,
+    bitwise one grid."""
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz, it = 4096, 12, 34, 9
+    ref = JacobiEngine(StencilSpec(dims=3, dtype="fp64", shape="star", kernel="direct"), nx, ny, nz, device=gpu)
+    ref.reset("random", 5)
+    fin, _ = ref.iterate(it)
+    want = ref.to_numpy(fin)
+    job = SlabJob(spec, nx, ny, nz, [gpu] * 2, exchange="copy", rolling=rolling, margin=12 if rolling else 0)
+    try:
+        job.fill_initial("random", 5)
+        job.run(it)
+        got = job.download()
+    finally:
+        job.close()
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
 def _rolling_copy_job(gpu, dtype, shape, nslabs, margin_extra=1):
     spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
     nx, ny, nz, it = 70, 45, 23 * nslabs + 1, 11
