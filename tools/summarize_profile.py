@@ -67,7 +67,7 @@ def main():
     sys.path.insert(0, ROOT)
     from bench import kernel_source_sha  # the sources the profiled library was built from
     for k, ent in summary["kernels"].items():
-        if "hbm_bytes_per_launch" in ent and k in ("temporalk", "temporal2", "zmarch", "direct", "boxk"):
+        if "hbm_bytes_per_launch" in ent and k in ("temporalk", "temporal2", "zmarch", "direct", "boxk", "tb2ds"):
             table.setdefault(workload, {})[k] = {"hbm_bytes_per_launch": round(ent["hbm_bytes_per_launch"]),
                                                  "source": f"profiles/{tag}_summary.json",
                                                  "kernel": ent["name"],
