@@ -61,7 +61,9 @@ int stencil_last_error(void);
  * the shape-sweep tests and A/B tools use.  Documented knobs, read by both:
  * STENCIL_TK_STEPS (3..5) / STENCIL_BOX_STEPS (3, 4) fused sweeps per launch,
  * STENCIL_TK_PACK / STENCIL_BOXK_PACK (0 equal z-chunks, 1 measured choice,
- * 2 the model's), STENCIL_SLAB_SIGNAL=0 (slab rounds without face signals). */
+ * 2 the model's), STENCIL_SLAB_SIGNAL=0 (slab rounds without face signals),
+ * STENCIL_SLAB_CPWAIT=1 (face-signalled slab rounds wait for the faces in the
+ * command processor, hipStreamWaitValue64, instead of a polling wait kernel). */
 int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */

@@ -183,12 +183,25 @@ struct HipDev {
         return stencil_sweepk(l, src, dst, b, e, k, s);
     }
     static int sweepk_signal(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k,
-                             uint32_t* counters, int* nsig, Stream s) {
+                             uint32_t* counters, uint64_t* fsig, int* nsig, Stream s) {
         int32_t n = 0;
-        const int rc = stencil_sweepk_signal(l, src, dst, b, e, k, counters, nullptr, &n, s);
+        const int rc = stencil_sweepk_signal(l, src, dst, b, e, k, counters, fsig, &n, s);
         *nsig = n;
         return rc;
     }
+    // STENCIL_SLAB_CPWAIT=1: face-signalled rounds gate the exchange on a HIP
+    // signal word waited on by the command processor (no wait kernel resident
+    // beside the launch); 0 (default): the polling wait kernel with its timeout
+    static int face_signal_create(uint64_t** fs) {
+        *fs = nullptr;
+        if (api_knob("STENCIL_SLAB_CPWAIT", 0) == 0) return STENCIL_OK;
+        if (int rc = stencil_face_signal_create(fs)) return rc;
+        if (int rc = stencil_face_signal_reset(*fs, nullptr)) return rc;
+        STENCIL_HIP_CHECK(hipDeviceSynchronize());
+        return STENCIL_OK;
+    }
+    static void face_signal_destroy(uint64_t* fs) { (void)stencil_face_signal_destroy(fs); }
+    static int wait_face_signal(uint64_t* fs, uint64_t target, Stream s) { return stencil_wait_face_signal(fs, target, s); }
     static int wait_counters(uint32_t* c, uint32_t lo, uint32_t hi, Stream s) {
         return stencil_wait_counters(c, lo, hi, c + 2, s);
     }

@@ -68,6 +68,11 @@ struct Slab {
     // on across launches), [2] the wait kernel's timeout flag
     uint32_t* counters = nullptr;
     uint32_t sig_target = 0;  // adds per face expected once the last queued launch is done
+    // STENCIL_SLAB_CPWAIT: the launch also adds 1 per completed face to this
+    // HIP signal word, and the exchange stream waits on it in the command
+    // processor (hipStreamWaitValue64) instead of a polling wait kernel
+    uint64_t* fsig = nullptr;
+    uint64_t fsig_target = 0;
 };
 
 template <class Dev>
@@ -318,11 +323,16 @@ int slab_round_signal(Job<Dev>& j, int k) {
         if (j.chained) SLAB_TRY(Dev::stream_wait(s.sb, s.ev_bnd));
         int nsig = 0;
         SLAB_TRY(time_begin(j, i, s.sb));
-        SLAB_TRY(Dev::sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, &nsig, s.sb));
+        SLAB_TRY(Dev::sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, s.fsig, &nsig, s.sb));
         SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, 1));
         SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
         s.sig_target += uint32_t(nsig);
-        SLAB_TRY(Dev::wait_counters(s.counters, s.sig_target, s.sig_target, s.sa));
+        if (s.fsig) {  // both faces of this launch: +2
+            s.fsig_target += 2;
+            SLAB_TRY(Dev::wait_face_signal(s.fsig, s.fsig_target, s.sa));
+        } else {
+            SLAB_TRY(Dev::wait_counters(s.counters, s.sig_target, s.sig_target, s.sa));
+        }
     }
     SLAB_TRY(exchange(j, dst_pos));
     for (Slab<Dev>& s : j.s) {
@@ -417,6 +427,7 @@ void release(JobT* j) {
         if (s.ev_int) Dev::event_destroy(s.ev_int);
         if (s.ev_join) Dev::event_destroy(s.ev_join);
         if (s.counters) Dev::free_counters(s.counters);
+        if (s.fsig) Dev::face_signal_destroy(s.fsig);
     }
     delete j;
 }
@@ -518,6 +529,7 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
             (rc = Dev::event_create(&s.ev_join, false)))
             break;
         if ((rc = Dev::alloc_counters(&s.counters))) break;
+        if (j->signal && (rc = Dev::face_signal_create(&s.fsig))) break;
     }
     if (rc != STENCIL_OK) {
         release<Dev>(j);

@@ -303,8 +303,14 @@ struct FakeDev {
                    ? sweep_t(l, static_cast<const double*>(src), static_cast<double*>(dst), b, e, k)
                    : sweep_t(l, static_cast<const float*>(src), static_cast<float*>(dst), b, e, k);
     }
+    static int face_signal_create(uint64_t** fs) {  // the fake waits synchronously: no signal word
+        *fs = nullptr;
+        return STENCIL_OK;
+    }
+    static void face_signal_destroy(uint64_t*) {}
+    static int wait_face_signal(uint64_t*, uint64_t, Stream) { return STENCIL_OK; }
     static int sweepk_signal(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k,
-                             uint32_t* counters, int* nsig, Stream s) {
+                             uint32_t* counters, uint64_t*, int* nsig, Stream s) {
         if (int rc = sweepk(l, src, dst, b, e, k, s)) return rc;
         {
             std::lock_guard<std::mutex> lk(fake::g_stat_mu);
