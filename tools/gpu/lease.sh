@@ -25,6 +25,7 @@
 #   zcab             tools/ab.py on 4096^2 x 512 fp64: z-chunk lengths (STENCIL_TK_ZCHUNK) of the wide-plane strip launch
 #   padscan:nx:ny:nz:sweeps[:dtype[:pad,pad..]]  tools/time_lib.py (debug library) over STENCIL_ROW_PAD values
 #   loop:<cfg>       bench.py --config <cfg> --exchange loopback (the whole grid as one periodic slab: an interior rank)
+#   slabgap          tools/slab_gap.py: one K = 4 launch plain / slab layout / halo flags / signalled / slab job
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
@@ -116,6 +117,8 @@ for step in "$@"; do
     loop:*) c=${step#loop:}
             timeout -k 10 300 python3 bench.py --config "$c" --exchange loopback --steps 40 --warmup 4 --no-cpu-baseline \
               > "$O/bench_${c}_loopback.json" 2>> "$O/bench.err" ;;
+    slabgap) timeout -k 10 300 python3 tools/slab_gap.py 4096 4096 512 > "$O/slab_gap.txt" 2>&1 &&
+             timeout -k 10 300 python3 tools/slab_gap.py 512 512 512 >> "$O/slab_gap.txt" 2>&1 ;;
     c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --order dma --variant 0 --variant 92416 >> "$O/c1_ab.txt" 2>&1 &&
           timeout -k 10 120 python3 tools/c1_ab.py --dtype fp32 --variant 0 --variant 92808 >> "$O/c1_ab.txt" 2>&1 ;;
