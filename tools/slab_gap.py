@@ -7,6 +7,7 @@ nx x ny x nz fp64, a -> b, timed with HIP events (best of --reps x 3 launches):
   halo4      the slab's layout (z ghost depth 4), no flags
   flags      halo4 + HALO_LO | HALO_HI (the slab's launch geometry)
   signal     flags as a face-signalled launch (stencil_sweepk_signal)
+  hipmalloc  flags on grids from stencil_alloc (hipMalloc) instead of torch
   slab       the C-ABI slab job: one periodic slab, face-signalled rounds
 
     python tools/slab_gap.py [nx ny nz] [--reps 5]"""
@@ -56,6 +57,21 @@ def main():
             out.append(("signal", ms))
         del e
         torch.cuda.empty_cache()
+    # the same launch on grids from hipMalloc (stencil_alloc, as the slab job allocates) instead of torch
+    import ctypes
+    lib = _lib.load()
+    lay = _lib.make_layout(StencilSpec(dims=3, dtype="fp64", halo=4).problem(nx, ny, nz, 3))
+    pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.check(lib.stencil_alloc(ctypes.byref(lay), ctypes.byref(pa)), "stencil_alloc", lib=lib)
+    _lib.check(lib.stencil_alloc(ctypes.byref(lay), ctypes.byref(pb)), "stencil_alloc", lib=lib)
+    for p_ in (pa, pb):
+        _lib.check(lib.stencil_fill_initial(ctypes.byref(lay), p_, _lib.INIT_RANDOM, 3, None), "fill", lib=lib)
+    ms = timed(lambda: _lib.check(lib.stencil_sweepk(ctypes.byref(lay), pa, pb, 0, nz, 4,
+                                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                                  "stencil_sweepk", lib=lib))
+    out.append(("hipmalloc", ms))
+    lib.stencil_free(pa)
+    lib.stencil_free(pb)
     job = SlabJob(StencilSpec(dims=3, dtype="fp64"), nx, ny, nz, [0], exchange="copy", periodic=True)
     job.fill_initial("random", 3)
     job.run(8)
