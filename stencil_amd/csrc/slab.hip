@@ -152,6 +152,8 @@ struct HipDev {
     static void free_counters(uint32_t* c) { (void)hipFree(c); }
     static int stream_create(Stream* s, bool high_priority) {
         int lo_prio = 0, hi_prio = 0;
+        // STENCIL_SLAB_NOPRIO=1 (debug library): both streams at the default priority
+        if (knob("STENCIL_SLAB_NOPRIO", 0)) high_priority = false;
         if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
             hipStreamCreateWithPriority(s, hipStreamNonBlocking, high_priority ? hi_prio : lo_prio) != hipSuccess)
             return set_error(STENCIL_EHIP, "stream creation failed");
