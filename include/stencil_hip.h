@@ -63,7 +63,9 @@ int stencil_last_error(void);
  * STENCIL_TK_PACK / STENCIL_BOXK_PACK (0 equal z-chunks, 1 measured choice,
  * 2 the model's), STENCIL_SLAB_SIGNAL=0 (slab rounds without face signals),
  * STENCIL_SLAB_CPWAIT=1 (face-signalled slab rounds wait for the faces in the
- * command processor, hipStreamWaitValue64, instead of a polling wait kernel). */
+ * command processor, hipStreamWaitValue64, instead of a polling wait kernel),
+ * STENCIL_SLAB_SERIAL=1 (every full slab round as one plain launch, then the
+ * exchange: nothing runs beside the launch). */
 int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */

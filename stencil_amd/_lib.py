@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libstencil_hip.so")
 # ones is set, i.e. by the shape-sweep tests and the A/B tools.
 DEBUG_LIB_PATH = os.path.join(_HERE, "libstencil_hip_debug.so")
 API_KNOBS = ("STENCIL_TK_STEPS", "STENCIL_BOX_STEPS", "STENCIL_TK_PACK", "STENCIL_BOXK_PACK", "STENCIL_SLAB_SIGNAL",
-             "STENCIL_SLAB_CPWAIT")
+             "STENCIL_SLAB_CPWAIT", "STENCIL_SLAB_SERIAL")
 
 STENCIL_OK = 0
 F32, F64 = 0, 1

@@ -115,6 +115,9 @@ struct HipDev {
         return 1;
     }
     static bool signal_enabled() { return api_knob("STENCIL_SLAB_SIGNAL", 1) != 0; }
+    // STENCIL_SLAB_SERIAL=1: every full round as one plain launch of the whole
+    // slab followed by the exchange (no overlap)
+    static bool serial_rounds() { return api_knob("STENCIL_SLAB_SERIAL", 0) != 0; }
     // STENCIL_SLAB_NO_PULL_WAIT=1 (debug library, the test that shows the
     // delay below exposing the race): drop the rolling exchange's wait
     static bool pull_wait_enabled() { return knob("STENCIL_SLAB_NO_PULL_WAIT", 0) == 0; }

@@ -85,6 +85,7 @@ struct Job {
     bool cur_is_a = true;
     bool chained = false;  // round events recorded since the last join
     bool signal = false;   // full rounds as face-signalled single launches
+    bool serial = false;   // full rounds as ONE plain launch, then the exchange (STENCIL_SLAB_SERIAL)
     int nranks = 0;        // rank mode: slabs of the job, this process owns s[0]
     // rolling (STENCIL_SLAB_ROLLING): spare planes below each slab's grid;
     // position 0 = the grid at home (allocation offset `margin` planes), 1 =
@@ -277,7 +278,10 @@ int slab_round(Job<Dev>& j, int k) {
             SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
         }
         const int64_t plane_cells = s.l.prob.nx * s.l.prob.ny;
-        if (s.n > 2 * edge) {
+        // serial rounds: the whole slab in one launch on A, the exchange
+        // behind it -- nothing runs beside the launch (an overlapped exchange's
+        // copy or RCCL kernels take CUs the one-per-CU strip grid counts on)
+        if (!j.serial && s.n > 2 * edge) {
             SLAB_TRY(time_begin(j, i, s.sb));
             SLAB_TRY(Dev::sweepk(&s.l, src, dst, edge, s.n - edge, k, s.sb));
             SLAB_TRY(time_end(j, i, s.sb, plane_cells * (s.n - 2 * edge), 1));
@@ -485,8 +489,9 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         bool distinct = true;
         for (size_t i = 0; i < devs.size(); ++i)
             for (size_t q = 0; q < i; ++q) distinct = distinct && devs[i] != devs[q];
+        j->serial = !rolling && Dev::serial_rounds();
         j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct && !rolling &&
-                    Dev::signal_enabled();
+                    !j->serial && Dev::signal_enabled();
     }
     const int64_t base = g.nz / total, rem = g.nz % total;
     // the smallest slab of the job decides, the same in every process: ranks

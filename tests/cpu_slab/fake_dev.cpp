@@ -303,6 +303,7 @@ struct FakeDev {
                    ? sweep_t(l, static_cast<const double*>(src), static_cast<double*>(dst), b, e, k)
                    : sweep_t(l, static_cast<const float*>(src), static_cast<float*>(dst), b, e, k);
     }
+    static bool serial_rounds() { return std::getenv("STENCIL_SLAB_SERIAL") && std::atoi(std::getenv("STENCIL_SLAB_SERIAL")); }
     static int face_signal_create(uint64_t** fs) {  // the fake waits synchronously: no signal word
         *fs = nullptr;
         return STENCIL_OK;

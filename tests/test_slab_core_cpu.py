@@ -81,6 +81,29 @@ def test_single_process_job_equals_one_grid(fake, dtype, shape, k, nslabs, excha
     job.close()
 
 
+@pytest.mark.parametrize("dtype,shape,k", SHAPES)
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("exchange", ["rccl", "copy"])
+def test_serial_rounds_equal_one_grid(fake, monkeypatch, dtype, shape, k, nslabs, exchange):
+    """STENCIL_SLAB_SERIAL=1: every full round as ONE plain launch of the
+    whole slab, then the exchange (no face signals, nothing beside the
+    launch); distinct devices, remainder rounds; bitwise."""
+    monkeypatch.setenv("STENCIL_SLAB_SERIAL", "1")
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz = 13, 7, 3 * k * nslabs + 2
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange=exchange, lib=fake)
+    job.fill_initial("random", 11)
+    sweeps = 0
+    for it in (2 * k + 1, k, 1, k - 1):
+        fake.stats(reset=True)
+        job.run(it)
+        sweeps += it
+        assert fake.stats()["signal_sweeps"] == 0
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps))
+    job.close()
+
+
 @pytest.mark.parametrize("nslabs", [1, 2, 3])
 @pytest.mark.parametrize("exchange", ["rccl", "copy"])
 def test_periodic_ring_equals_replicated_grid(fake, nslabs, exchange):
