@@ -614,6 +614,7 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
                        "slab job (stencil_slab_create_rank), RCCL send/recv between the ranks' slabs" +
                        (f"; ONE grid per slab + a rolling margin of {roll['margin']} planes" if roll["margin"] else ""))
         form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
+            "serial launches (whole slab, then the exchange)" if kt.get("serial") else \
             "boundary + interior launches"
         line = report(args, pre, spec, kname, plan["grid"], world, elapsed, kt["total_ms"] / max(1, kt["launches"]),
                       float(kt["cells_per_launch"]), res["k"], kt["launches"], parallelism,
@@ -686,6 +687,7 @@ def main_slab_job(args):
     check = None if sums is None else global_grid_check(spec, plan["grid"], sweeps, sums, 0, init=args.init)
     kname = "boxk" if spec.shape == "box" else "temporalk"
     form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
+            "serial launches (whole slab, then the exchange)" if kt.get("serial") else \
         "boundary + interior launches"
     if loop:
         parallelism = ("1 GPU rehearsing an interior rank" +

@@ -395,7 +395,7 @@ int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
  * z-range launches in rolling rounds) on that launch's stream.  kernel_time
  * synchronises and returns the summed device time, the spans timed, the
  * interior cells one span covers and the round form (0 boundary + interior,
- * 1 face-signalled, 2 rolling).  Enabling (or disabling) drops earlier
+ * 1 face-signalled, 2 rolling, 3 serial).  Enabling (or disabling) drops earlier
  * records. */
 int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
 int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,

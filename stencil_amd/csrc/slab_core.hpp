@@ -784,7 +784,7 @@ int kernel_time(JobT* job, float* total_ms, int64_t* launches, int64_t* cells_pe
     // per span, so `cells_per_launch` is what one span covers
     if (launches) *launches = int64_t(job->tev.size());
     if (cells_per_launch) *cells_per_launch = job->timed_cells;
-    if (signalled) *signalled = job->signal ? 1 : job->margin ? 2 : 0;
+    if (signalled) *signalled = job->signal ? 1 : job->margin ? 2 : job->serial ? 3 : 0;
     clear_error();
     return STENCIL_OK;
 }

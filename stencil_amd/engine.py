@@ -453,9 +453,9 @@ class SlabJob:
         ms, n, cells, sig = ctypes.c_float(0.0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
         _lib.check(self.lib.stencil_slab_kernel_time(self.job, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(cells),
                                                      ctypes.byref(sig)), "stencil_slab_kernel_time", lib=self.lib)
-        # the round form: 0 boundary + interior launches, 1 face-signalled, 2 rolling passes
+        # the round form: 0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial
         return {"total_ms": float(ms.value), "launches": int(n.value), "cells_per_launch": int(cells.value),
-                "signalled": int(sig.value) == 1, "rolling": int(sig.value) == 2}
+                "signalled": int(sig.value) == 1, "rolling": int(sig.value) == 2, "serial": int(sig.value) == 3}
 
     def plane_sums(self) -> np.ndarray:
         out = np.zeros(self.shape[2], dtype=np.float64)
