@@ -119,6 +119,8 @@ for step in "$@"; do
               > "$O/bench_${c}_loopback.json" 2>> "$O/bench.err" ;;
     slabgap) timeout -k 10 300 python3 tools/slab_gap.py 4096 4096 512 > "$O/slab_gap.txt" 2>&1 &&
              timeout -k 10 300 python3 tools/slab_gap.py 512 512 512 >> "$O/slab_gap.txt" 2>&1 ;;
+    slabtrace) (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O/slabtrace" -o run -- \
+                 python3 "$R/tools/slab_gap.py" 512 512 512 --reps 3 > "$O/slabtrace.log" 2>&1) ;;
     slabgapnp) STENCIL_SLAB_NOPRIO=1 timeout -k 10 300 python3 tools/slab_gap.py 4096 4096 512 > "$O/slab_gap_noprio.txt" 2>&1 &&
              STENCIL_SLAB_NOPRIO=1 timeout -k 10 300 python3 tools/slab_gap.py 512 512 512 >> "$O/slab_gap_noprio.txt" 2>&1 ;;
     c1ab) timeout -k 10 120 python3 tools/c1_ab.py --dtype fp64 --variant 0 --variant 92416 > "$O/c1_ab.txt" 2>&1 &&
