@@ -140,6 +140,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
                     help="N>1: skip the bitwise check against the global grid run as one grid on rank 0")
+    ap.add_argument("--slab-timeout-ms", type=int, default=0,
+                    help="N>1 / rehearsals: the slab job's deadline for any device wait (stencil_slab_set_timeout; "
+                         "0 = the library's default, 60 s): past it the job aborts its communicators and bench.py "
+                         "exits non-zero")
     ap.add_argument("--allow-debug-library", action="store_true",
                     help="bench even when an experiment knob (a STENCIL_* variable the product ignores) is set, "
                          "i.e. on libstencil_hip_debug.so; the JSON line names the library and the knobs either way")
@@ -347,6 +351,38 @@ def reference_plane_sums(spec, grid, sweeps, device, force_reduced=False, init="
                         "middle plane, the others its plane as far from the same end)")
 
 
+def periodic_slab_check(spec, grid, sweeps, got, device, init="reference"):
+    """A rehearsal's periodic slab (its halos its own faces) from the
+    reference initial condition, which is z-uniform: every plane stays equal
+    to every other (bitwise) and to the middle plane of a (2t + 1)-plane grid
+    run as one grid for the same sweeps, which no z end reaches.  The second
+    half is skipped (and said so) when that grid does not fit."""
+    import numpy as np
+    import torch
+    if init != "reference":
+        return {"skipped": "the periodic check needs the z-uniform reference initial condition"}
+    gnx, gny, gnz = grid
+    bits = got.view(np.uint64)
+    out = {"planes": int(gnz), "sweeps": int(sweeps),
+           "planes_differing_from_plane_0": int(np.count_nonzero(bits != bits[0]))}
+    t = int(sweeps) * spec.radius
+    need = 2.2 * gnx * gny * (2 * t + 1) * spec.elem_bytes
+    if need > 0.8 * torch.cuda.mem_get_info(device)[0]:
+        out["reference"] = f"z-uniformity only: the {2 * t + 1}-plane one-grid reference does not fit"
+        out["bitwise_equal"] = out["planes_differing_from_plane_0"] == 0
+        return out
+    try:
+        want, _ = reference_plane_sums(spec, (gnx, gny, 2 * t + 1), sweeps, device)
+        mid = want[t:t + 1].view(np.uint64)[0]
+        out["planes_differing"] = int(np.count_nonzero(bits != mid))
+        out["bitwise_equal"] = out["planes_differing"] == 0
+        out["reference"] = (f"every plane against the middle plane of a {2 * t + 1}-plane grid run as one grid on "
+                            f"GPU {device} (no z end reaches it in {sweeps} sweeps)")
+    except Exception as exc:  # a check, never the measurement
+        out["error"] = f"{type(exc).__name__}: {exc}"[:300]
+    return out
+
+
 def global_grid_check(spec, grid, sweeps, got, device, init="reference"):
     """The multi-GPU job's per-plane sums `got` against the same sweeps of one
     grid on `device` (reference_plane_sums), bit for bit."""
@@ -408,8 +444,9 @@ def main_single(args):
         elapsed = time.perf_counter() - t0
         kernel_ms_total = dev_ms
         cells_per_launch = float(gnx) * gny * gnz  # charged per pass of K sweeps over the whole grid
-        extra = {"rolling": {"shift_planes": shift, "launch_planes": shift - sweeps_per_launch,
-                             "launches": kernel_launches, "grid_bytes": grid.bytes}}
+        extra = dict(settle_config(0, 0.0, "none beyond the warm-up sweeps"),
+                     rolling={"shift_planes": shift, "launch_planes": shift - sweeps_per_launch,
+                              "launches": kernel_launches, "grid_bytes": grid.bytes})
         kernels_per_launch = kernel_launches / max(1.0, args.steps / sweeps_per_launch)
         del grid
         torch.cuda.empty_cache()  # the copy-kernel calibration needs 2 GiB
@@ -428,7 +465,7 @@ def main_single(args):
         # settle the one-time per-shape choice (packed vs equal z-chunks, timed
         # on the first launch of a shape) outside the timed region whatever W
         # is: one fused launch a -> b, grid a unchanged
-        eng.prepare()
+        settle = eng.prepare()
         eng.iterate(args.warmup)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -437,7 +474,9 @@ def main_single(args):
         elapsed = time.perf_counter() - t0
         kernel_launches = eng.plan(args.steps)[0]
         cells_per_launch = float(gnx) * gny * gnz
-        extra, kernels_per_launch = None, 1.0
+        extra, kernels_per_launch = settle_config(settle["launches"], settle["device_ms"],
+                                                  "stencil_prepare2: the schedule trial + ~25 ms of the job's own "
+                                                  "launch (a -> b, grid a unchanged)"), 1.0
         parallelism = "1 GPU, one process, the whole grid (no decomposition)"
         timing = "hipEvents of stencil_iterate over the timed region"
         key = f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz}"
@@ -467,7 +506,7 @@ def main_2d(args):
     eng = JacobiEngine(spec, nx, ny, 1, device=0)
     eng.reset(args.init, INIT_SEED)
     launches, _ = eng.plan(args.steps)
-    eng.prepare()  # untimed settle (a -> b, grid a unchanged): ~25 ms of launches, as every other driver
+    settle = eng.prepare()  # untimed settle (a -> b, grid a unchanged): ~25 ms of launches, as every other driver
     eng.iterate(args.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -480,8 +519,10 @@ def main_2d(args):
            launches, "1 GPU, one process, the whole grid", rounds=None,
            launch_timing="hipEvents of stencil_iterate over the timed region", workload_key="C1_2d_1024",
            local=0, check=None, cpu=True,
-           extra_config={"us_per_sweep_device": round(dev_ms * 1e3 / max(1, args.steps), 3),
-                         "bound": "launch + per-sweep barrier latency (a 16.8 MB grid; DESIGN.md §5, §9.3)"},
+           extra_config=dict(settle_config(settle["launches"], settle["device_ms"],
+                                           "stencil_prepare2: ~25 ms of the job's own K-sweep launch"),
+                             us_per_sweep_device=round(dev_ms * 1e3 / max(1, args.steps), 3),
+                             bound="launch + per-sweep barrier latency (a 16.8 MB grid; DESIGN.md §5, §9.3)"),
            cpu_full=True)
 
 
@@ -493,21 +534,28 @@ def _slab_spec(args, pre):
 SETTLE_MS = 25.0  # as stencil_prepare: the GPU's clock settles over ~15 ms of heavy launches after idling
 
 
+def settle_config(launches, ms, what):
+    """What ran before the timed region besides the W warm-up steps (the
+    line's `warmup` counts only those): the settle's launches (or rounds) and
+    their time, DESIGN.md §6."""
+    return {"settle_launches": int(launches), "settle_ms": round(float(ms), 3), "settle": what}
+
+
 def settle_rounds(job, k, rounds=None):
     """Untimed rounds for about SETTLE_MS (at most 64 rounds): `rounds` of
-    them, or -- one process -- as many as one timed round says fit; returns
-    the sweeps run (the check counts them).  Ranks of one job must run the
-    same rounds (every round exchanges halos): they pass `rounds` from
-    settle_rounds_for(), which depends only on the global problem."""
+    them, or -- one process -- as many as one timed round says fit.  Returns
+    (sweeps run -- the check counts them --, rounds, host ms).  Ranks of one
+    job must run the same rounds (every round exchanges halos): they pass
+    `rounds` from settle_rounds_for(), which depends only on the global
+    problem."""
     if rounds is None:
         ms = job.run(k)
         n = int(min(64, SETTLE_MS / ms)) if ms > 0 else 0
         if n:
-            job.run(n * k)
-        return k * (n + 1)
-    if rounds:
-        job.run(rounds * k)
-    return rounds * k
+            ms += job.run(n * k)
+        return k * (n + 1), n + 1, ms
+    ms = job.run(rounds * k) if rounds else 0.0
+    return rounds * k, rounds, ms
 
 
 def settle_rounds_for(grid, world, k, rate_gcell=1000.0):
@@ -527,6 +575,8 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
     gnx, gny, gnz = grid
     job = SlabJob(spec, gnx, gny, gnz, [device], rank=(world, rank, uid), rolling=rolling, margin=0, lib=lib)
     try:
+        if args.slab_timeout_ms:
+            job.set_timeout(args.slab_timeout_ms)
         info = job.info(0)
         roll = job.rolling_info()
         k = info["sweeps_per_round"]
@@ -535,7 +585,8 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
         job.run(k + 1)  # a full and a remainder round: both launch paths' one-time costs
         if barrier:
             barrier()
-        sweeps += settle_rounds(job, k, settle_rounds_for(grid, world, k))  # the same rounds on every rank
+        settled = settle_rounds(job, k, settle_rounds_for(grid, world, k))  # the same rounds on every rank
+        sweeps += settled[0]
         job.run(args.warmup)
         if barrier:
             barrier()
@@ -548,7 +599,8 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
         job.kernel_timing(False)
         sweeps += extra
         sums = None if args.no_check else job.plane_sums()[info["first"]:info["first"] + info["planes"]].copy()
-        return {"info": info, "rolling": roll, "k": k, "elapsed": elapsed, "kt": kt, "sweeps": sweeps, "sums": sums}
+        return {"info": info, "rolling": roll, "k": k, "elapsed": elapsed, "kt": kt, "sweeps": sweeps, "sums": sums,
+                "settle": settled}
     finally:
         job.close()
 
@@ -624,7 +676,10 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
                                     f"{args.config}_slab_{res['info']['planes']}_x{world}"),
                       local=local, check=check if on_gpu else {"skipped": "no GPU (CPU rehearsal)"}, cpu=False,
                       kernels_per_launch=float(max(1, roll["launches_per_pass"])) if roll["margin"] else 1.0,
-                      extra_config={"slab_plan": {k: v for k, v in plan.items() if k != "grid"}},
+                      extra_config=dict(settle_config(res["settle"][1], res["settle"][2],
+                                                      "untimed full rounds (the same count on every rank), after one "
+                                                      "full and one remainder round"),
+                                        slab_plan={k: v for k, v in plan.items() if k != "grid"}),
                       calibrate=on_gpu, emit=on_gpu)
         return line, got, res
     return None, got, res
@@ -665,6 +720,8 @@ def main_slab_job(args):
     spec = _slab_spec(args, pre)
     gnx, gny, gnz = plan["grid"]
     job = SlabJob(spec, gnx, gny, gnz, devices, exchange=exchange, periodic=loop, rolling=plan["rolling"], margin=0)
+    if args.slab_timeout_ms:
+        job.set_timeout(args.slab_timeout_ms)
     job.fill_initial(args.init, INIT_SEED)
     k = job.info(0)["sweeps_per_round"]
     roll = job.rolling_info()
@@ -672,7 +729,8 @@ def main_slab_job(args):
     # the one-time costs of both launch paths (schedule trials, first launches)
     sweeps = k + 1 + args.warmup
     job.run(k + 1)
-    sweeps += settle_rounds(job, k)
+    settled = settle_rounds(job, k)
+    sweeps += settled[0]
     job.run(args.warmup)
     elapsed = job.run(args.steps) * 1e-3  # host wall time, every device synchronised at both ends
     sweeps += args.steps
@@ -682,9 +740,14 @@ def main_slab_job(args):
     kt = job.kernel_time()
     job.kernel_timing(False)
     sweeps += extra
-    sums = job.plane_sums() if not (args.no_check or loop) else None
+    sums = job.plane_sums() if not args.no_check else None
     job.close()
-    check = None if sums is None else global_grid_check(spec, plan["grid"], sweeps, sums, 0, init=args.init)
+    if sums is None:
+        check = None
+    elif loop:
+        check = periodic_slab_check(spec, plan["grid"], sweeps, sums, 0, init=args.init)
+    else:
+        check = global_grid_check(spec, plan["grid"], sweeps, sums, 0, init=args.init)
     kname = "boxk" if spec.shape == "box" else "temporalk"
     form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
             "serial launches (whole slab, then the exchange)" if kt.get("serial") else \
@@ -710,6 +773,9 @@ def main_slab_job(args):
            local=0, check=check if n_gpus > 1 else None, cpu=False,
            kernels_per_launch=float(max(1, roll["launches_per_pass"])) if roll["margin"] else 1.0,
            extra_config=dict({"slab_plan": {k2: v for k2, v in plan.items() if k2 != "grid"}},
+                             **settle_config(settled[1], settled[2], "untimed full rounds after one full and one "
+                                                                    "remainder round"),
+                             **({"rehearsal_check": check} if loop else {}),
                              **({"rank_of": args.rank_of, "global_grid": list(rank_plan["grid"])} if args.rank_of
                                 else {})))
 
@@ -759,7 +825,10 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
             "grid": [gnx, gny, gnz] if pre.get("dims", 3) == 3 else [gnx, gny],
             "kernel": kname,
             "parallelism": parallelism,
-            "achieved_hbm_GBps_whole_job": round(gcell * bytes_per_update, 1),
+            # SURVEY 8(d)'s algorithmic bytes (2 x sizeof(T) per cell-update) at the
+            # whole job's rate: K fused sweeps per launch put it above the HBM
+            # peak; the roofline's `achieved` is the HBM-side (compulsory) figure
+            "effective_GBps_whole_job": round(gcell * bytes_per_update, 1),
             "rounds": rounds,
             **library_info(),
         },

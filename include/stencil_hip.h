@@ -51,6 +51,7 @@ extern "C" {
 #define STENCIL_ENOMEM (-3)      /* device allocation failed */
 #define STENCIL_ENODEV (-4)      /* no usable gfx950 device */
 #define STENCIL_EUNSUPPORTED (-5)
+#define STENCIL_ETIMEOUT (-6)      /* a slab job's device wait passed its deadline (a peer stopped answering) */
 
 const char* stencil_strerror(int code);
 const char* stencil_last_error_message(void);
@@ -65,7 +66,12 @@ int stencil_last_error(void);
  * STENCIL_SLAB_CPWAIT=1 (face-signalled slab rounds wait for the faces in the
  * command processor, hipStreamWaitValue64, instead of a polling wait kernel),
  * STENCIL_SLAB_SERIAL=1 (every full slab round as one plain launch, then the
- * exchange: nothing runs beside the launch). */
+ * exchange: nothing runs beside the launch), STENCIL_SLAB_XCU=c (the slab
+ * exchange's stream confined to c CUs of every XCD, 0 = not confined) and
+ * STENCIL_SLAB_XCU_EXCL=1 (the launches' streams kept off those CUs),
+ * STENCIL_SLAB_TIMEOUT_MS (a slab job's deadline for any device wait,
+ * default 60000: stencil_slab_set_timeout), STENCIL_SLAB_ROLLING_OVERLAP=0
+ * (rolling slab rounds exchange after the pass instead of beside it). */
 int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */
@@ -263,6 +269,11 @@ int stencil_iterate(const stencil_layout* l, void* a, void* b, uint32_t iteratio
  * Blocks the host once.  A no-op for jobs without a K-step launch.  No
  * reference counterpart (the reference has no per-shape state). */
 int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream);
+/* The same, reporting what ran before the caller's timed region: the kernel
+ * launches (the schedule trial's included) and their device time, estimated
+ * from the one timed settle launch. */
+int stencil_prepare2(const stencil_layout* l, const void* a, void* b, void* stream, int64_t* settle_launches,
+                     float* settle_ms);
 
 /* One resident grid instead of two (3D, no slab flags): for jobs whose two
  * ping-pong grids do not fit the GPU -- BASELINE config 3, 4096^3 fp32, is
@@ -337,7 +348,12 @@ enum { STENCIL_EXCHANGE_RCCL = 0, STENCIL_EXCHANGE_COPY = 1 };
  * stencil_rolling_*, per slab): a round is a pass of ceil(n / S) z-range
  * launches (S = margin - K*radius), then the exchange -- for slabs whose two
  * grids do not fit one GPU, e.g. the north star's 4096^3 fp64 on 2 GPUs (one
- * 278 GB grid each).  Bitwise the two-grid job; no face-signalled rounds. */
+ * 278 GB grid each).  Bitwise the two-grid job; no face-signalled rounds.
+ * No sweep writes a ghost cell, and a pass lands each plane in a slot whose
+ * x/y ghost ring came from another plane, so a ROLLING job needs the same
+ * x/y ghost ring in every plane and equal bottom ghost planes (the reference
+ * initial condition has both): stencil_slab_upload checks a host grid for
+ * this and returns STENCIL_EINVAL otherwise. */
 enum { STENCIL_SLAB_PERIODIC = 1, STENCIL_SLAB_ROLLING = 2 };
 typedef struct stencil_slab_job stencil_slab_job;
 
@@ -380,7 +396,8 @@ int stencil_slab_rolling_info(const stencil_slab_job* job, int64_t* margin_plane
  * interior, as stencil_fill_initial on one grid), halos exchanged. */
 int stencil_slab_fill_initial(stencil_slab_job* job, int32_t init_kind, uint64_t seed);
 /* The global grid from / to a dense host array with ghosts (x fastest,
- * host_row elements per row, host_rows rows per plane, nz + 2r planes). */
+ * host_row elements per row, host_rows rows per plane, nz + 2r planes).
+ * ROLLING jobs: see the ghost-ring condition above. */
 int stencil_slab_upload(stencil_slab_job* job, const void* host, int64_t host_row, int64_t host_rows);
 int stencil_slab_download(stencil_slab_job* job, void* host, int64_t host_row, int64_t host_rows);
 /* `iterations` sweeps of the whole job (rounds of K, the remainder as one
@@ -394,12 +411,33 @@ int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
  * rounds, its interior launch in boundary + interior rounds, the pass's
  * z-range launches in rolling rounds) on that launch's stream.  kernel_time
  * synchronises and returns the summed device time, the spans timed, the
- * interior cells one span covers and the round form (0 boundary + interior,
- * 1 face-signalled, 2 rolling, 3 serial).  Enabling (or disabling) drops earlier
- * records. */
+ * interior cells one span covers and whether the rounds are face-signalled
+ * (1) or not (0); stencil_slab_round_form gives the form.  Enabling (or
+ * disabling) drops earlier records. */
 int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
 int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,
                              int32_t* signalled);
+/* The form of the job's full rounds (kernel_time's `signalled` is 1 for
+ * face-signalled rounds, 0 otherwise). */
+enum {
+    STENCIL_SLAB_FORM_BOUNDARY_INTERIOR = 0, /* boundary planes on one stream, the interior on another */
+    STENCIL_SLAB_FORM_SIGNALLED = 1,         /* one face-signalled launch, the exchange as the faces land */
+    STENCIL_SLAB_FORM_ROLLING = 2,           /* one grid + a margin: a pass of z-range launches */
+    STENCIL_SLAB_FORM_SERIAL = 3             /* one launch of the whole slab, then the exchange */
+};
+int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form);
+/* Bounded-time failure.  Every wait of the job for its devices (the end of
+ * run(), fill, upload, download, plane sums, and -- while run() issues
+ * rounds -- the exchange of the round kInflight = 8 rounds back) gives up
+ * after `timeout_ms` (default 60000, or the STENCIL_SLAB_TIMEOUT_MS knob at
+ * creation); so does an asynchronous RCCL error, polled meanwhile
+ * (ncclCommGetAsyncError).  The job then aborts its communicators
+ * (ncclCommAbort: RCCL's kernels waiting for a peer that stopped posting
+ * return), releases its queued face waits, and the call returns
+ * STENCIL_ETIMEOUT (or the error); every later call on the job fails, and
+ * stencil_slab_destroy frees it.  The reference has no counterpart: its
+ * never-waited reply (stencil_rma.cpp:334-338) hangs instead. */
+int stencil_slab_set_timeout(stencil_slab_job* job, int64_t timeout_ms);
 
 #ifdef __cplusplus
 }

@@ -17,9 +17,12 @@ LIB_PATH = os.path.join(_HERE, "libstencil_hip.so")
 # ones is set, i.e. by the shape-sweep tests and the A/B tools.
 DEBUG_LIB_PATH = os.path.join(_HERE, "libstencil_hip_debug.so")
 API_KNOBS = ("STENCIL_TK_STEPS", "STENCIL_BOX_STEPS", "STENCIL_TK_PACK", "STENCIL_BOXK_PACK", "STENCIL_SLAB_SIGNAL",
-             "STENCIL_SLAB_CPWAIT", "STENCIL_SLAB_SERIAL")
+             "STENCIL_SLAB_CPWAIT", "STENCIL_SLAB_SERIAL", "STENCIL_SLAB_XCU", "STENCIL_SLAB_XCU_EXCL",
+             "STENCIL_SLAB_TIMEOUT_MS", "STENCIL_SLAB_ROLLING_OVERLAP")
 
 STENCIL_OK = 0
+ETIMEOUT = -6
+SLAB_FORMS = {0: "boundary + interior", 1: "face-signalled", 2: "rolling", 3: "serial"}
 F32, F64 = 0, 1
 STAR, BOX = 0, 1
 ORDER_NAIVE, ORDER_DMA = 0, 1
@@ -48,7 +51,8 @@ EXPORTED_SYMBOLS = (
     "stencil_slab_create", "stencil_slab_destroy", "stencil_slab_info", "stencil_slab_fill_initial",
     "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
     "stencil_slab_kernel_timing", "stencil_slab_kernel_time", "stencil_slab_unique_id", "stencil_slab_create_rank",
-    "stencil_slab_create2", "stencil_slab_create_rank2", "stencil_slab_rolling_info",
+    "stencil_slab_create2", "stencil_slab_create_rank2", "stencil_slab_rolling_info", "stencil_slab_round_form",
+    "stencil_slab_set_timeout", "stencil_prepare2",
 )
 
 
@@ -142,6 +146,7 @@ def signatures() -> dict:
         "stencil_sweepk": (c_int, [L, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
         "stencil_iterate": (c_int, [L, c_void_p, c_void_p, c_uint32, c_void_p, POINTER(c_int), POINTER(c_float)]),
         "stencil_prepare": (c_int, [L, c_void_p, c_void_p, c_void_p]),
+        "stencil_prepare2": (c_int, [L, c_void_p, c_void_p, c_void_p, POINTER(c_int64), POINTER(c_float)]),
         "stencil_rolling_bytes": (c_int, [L, c_int64, POINTER(c_int64), POINTER(c_int32)]),
         "stencil_rolling_init_margin": (c_int, [L, c_void_p, c_int64, c_void_p]),
         "stencil_rolling_iterate": (c_int, [L, c_void_p, c_int64, c_uint32, POINTER(c_int32), c_void_p,
@@ -182,6 +187,8 @@ def signatures() -> dict:
         "stencil_slab_kernel_timing": (c_int, [c_void_p, c_int32]),
         "stencil_slab_kernel_time": (c_int, [c_void_p, POINTER(c_float), POINTER(c_int64), POINTER(c_int64),
                                              POINTER(c_int32)]),
+        "stencil_slab_round_form": (c_int, [c_void_p, POINTER(c_int32)]),
+        "stencil_slab_set_timeout": (c_int, [c_void_p, c_int64]),
     }
 
 

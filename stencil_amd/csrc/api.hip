@@ -275,6 +275,8 @@ __global__ void __launch_bounds__(64) wait_counters_kernel(const uint32_t* __res
         const uint32_t a = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t b = __hip_atomic_load(&c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a >= tlo && b >= thi) return;
+        // the host sets the flag to release a wait (a slab job that failed)
+        if (__hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
         if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(1000) * 1000 * 1000) {
             __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
@@ -314,6 +316,7 @@ const char* stencil_strerror(int code) {
     case STENCIL_ENOMEM: return "out of device memory";
     case STENCIL_ENODEV: return "no usable GPU";
     case STENCIL_EUNSUPPORTED: return "unsupported combination";
+    case STENCIL_ETIMEOUT: return "a device wait passed its deadline";
     default: return "unknown error";
     }
 }
@@ -673,6 +676,13 @@ constexpr float kSettleMs = 25.f;
 constexpr float kSettleMaxLaunches = 2048.f;  // a 14-us C1 launch needs ~1800 for 25 ms
 
 int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* stream) {
+    return stencil_prepare2(l, a, b, stream, nullptr, nullptr);
+}
+
+int stencil_prepare2(const stencil_layout* l, const void* a, void* b, void* stream, int64_t* settle_launches,
+                     float* settle_ms) {
+    if (settle_launches) *settle_launches = 0;
+    if (settle_ms) *settle_ms = 0.f;
     if (int rc = check_layout(l)) return rc;
     if (!a || !b || a == b) return set_error(STENCIL_EINVAL, "need two distinct grids");
     hipStream_t s = as_stream(stream);
@@ -707,6 +717,10 @@ int stencil_prepare(const stencil_layout* l, const void* a, void* b, void* strea
     if (e != hipSuccess) return set_error(STENCIL_EHIP, "prepare: %s", hipGetErrorString(e));
     const int more = ms > 0.f ? int(std::min(kSettleMaxLaunches, kSettleMs / ms)) : 0;
     for (int i = 0; i < more && rc == STENCIL_OK; ++i) rc = launch();
+    // what ran before the caller's timed region: the trial launch, the timed
+    // one and `more` (their device time estimated from the timed one)
+    if (settle_launches) *settle_launches = 2 + more;
+    if (settle_ms) *settle_ms = ms * float(2 + more);
     if (rc == STENCIL_OK) clear_error();
     return rc;
 }

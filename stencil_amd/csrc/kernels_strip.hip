@@ -546,17 +546,19 @@ __global__ void __launch_bounds__(64 * NW)
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     const unsigned ntiles = unsigned(tiles_x) * unsigned(tiles_y);
-                    bool last = false;
+                    // faces this workgroup completed (0, 1 or 2: a one-chunk
+                    // slab of K planes stores both faces at the same step)
+                    unsigned long long done = 0;
                     if (lo_here)
-                        last |= (__hip_atomic_fetch_add(&sig[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                        done += (__hip_atomic_fetch_add(&sig[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
                                     ntiles == 0;
                     if (hi_here)
-                        last |= (__hip_atomic_fetch_add(&sig[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
+                        done += (__hip_atomic_fetch_add(&sig[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1) %
                                     ntiles == 0;
-                    if (fsig && last) {
+                    if (fsig && done) {
                         // every add of this face came after its workgroup's release
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                        __hip_atomic_fetch_add(fsig, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_fetch_add(fsig, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
             }

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -34,7 +35,7 @@ namespace {
 
 // ---- the few RCCL entry points used, resolved at run time -----------------
 typedef struct ncclComm* ncclComm_t;
-typedef enum { ncclSuccess = 0 } ncclResult_t;
+typedef enum { ncclSuccess = 0, ncclInProgress = 7 } ncclResult_t;
 struct ncclUniqueId { char internal[128]; };  // NCCL_UNIQUE_ID_BYTES
 enum { ncclChar = 0, ncclUint8 = 1 };  // ncclDataType_t: bytes
 
@@ -43,6 +44,8 @@ struct Rccl {
     ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*Send)(const void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
@@ -63,12 +66,15 @@ const Rccl& rccl() {
         sym(r.GetUniqueId, "ncclGetUniqueId");
         sym(r.CommInitRank, "ncclCommInitRank");
         sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.CommAbort, "ncclCommAbort");
+        sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
         sym(r.GroupStart, "ncclGroupStart");
         sym(r.GroupEnd, "ncclGroupEnd");
         sym(r.Send, "ncclSend");
         sym(r.Recv, "ncclRecv");
         sym(r.GetErrorString, "ncclGetErrorString");
-        r.ok = r.CommInitAll && r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.GroupStart && r.GroupEnd && r.Send && r.Recv && r.GetErrorString;
+        r.ok = r.CommInitAll && r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.CommAbort && r.CommGetAsyncError &&
+               r.GroupStart && r.GroupEnd && r.Send && r.Recv && r.GetErrorString;
     });
     return r;
 }
@@ -118,6 +124,9 @@ struct HipDev {
     // STENCIL_SLAB_SERIAL=1: every full round as one plain launch of the whole
     // slab followed by the exchange (no overlap)
     static bool serial_rounds() { return api_knob("STENCIL_SLAB_SERIAL", 0) != 0; }
+    // STENCIL_SLAB_ROLLING_OVERLAP=0: rolling rounds exchange after the pass
+    // (slab_round_rolling) instead of beside it (slab_round_rolling_overlap)
+    static bool rolling_overlap() { return api_knob("STENCIL_SLAB_ROLLING_OVERLAP", 1) != 0; }
     // STENCIL_SLAB_NO_PULL_WAIT=1 (debug library, the test that shows the
     // delay below exposing the race): drop the rolling exchange's wait
     static bool pull_wait_enabled() { return knob("STENCIL_SLAB_NO_PULL_WAIT", 0) == 0; }
@@ -153,9 +162,67 @@ struct HipDev {
         return STENCIL_OK;
     }
     static void free_counters(uint32_t* c) { (void)hipFree(c); }
-    static int stream_create(Stream* s, bool high_priority) {
+    // the wait kernel's timeout flag in host-coherent memory: the host can
+    // release a queued wait by writing it, whatever the device queues hold
+    static int alloc_flag(uint32_t** f) {
+        if (hipHostMalloc(reinterpret_cast<void**>(f), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+            return set_error(STENCIL_EHIP, "timeout flag");
+        __atomic_store_n(*f, 0u, __ATOMIC_SEQ_CST);
+        return STENCIL_OK;
+    }
+    static void free_flag(uint32_t* f) { (void)hipHostFree(f); }
+    // counters, flag and face signal back to 0 (the streams are idle)
+    static int reset_counters(uint32_t* c, uint32_t* flag, uint64_t* fs) {
+        if (c) STENCIL_HIP_CHECK(hipMemset(c, 0, 4 * sizeof(uint32_t)));
+        if (flag) __atomic_store_n(flag, 0u, __ATOMIC_SEQ_CST);
+        if (fs) {
+            if (int rc = stencil_face_signal_reset(fs, nullptr)) return rc;
+            STENCIL_HIP_CHECK(hipDeviceSynchronize());
+        }
+        return STENCIL_OK;
+    }
+    // a failed job: let every queued face wait return (the polling kernel
+    // sees the flag; a command-processor wait sees its target passed)
+    static void release_waits(uint32_t* flag, uint64_t* fs) {
+        if (flag) __atomic_store_n(flag, 1u, __ATOMIC_SEQ_CST);
+        if (fs) {
+            hipPointerAttribute_t a{};
+            if (hipPointerGetAttributes(&a, fs) == hipSuccess && a.hostPointer)
+                __atomic_store_n(static_cast<uint64_t*>(a.hostPointer), uint64_t(1) << 62, __ATOMIC_SEQ_CST);
+            (void)hipGetLastError();
+        }
+    }
+    // A slab's streams by role (slab_core.hpp StreamRole): boundary launches
+    // at high priority, the interior / whole-slab launches, the exchange.
+    // STENCIL_SLAB_XCU=c (c CUs per XCD, 0 = off): the exchange stream is
+    // confined to c CUs of every XCD (hipExtStreamCreateWithCUMask), so
+    // RCCL's and the copies' kernels run there and not on the CUs a
+    // one-per-CU launch beside them counts on; STENCIL_SLAB_XCU_EXCL=1 also
+    // keeps the launches' streams off those CUs.
+    static int xcu() { return std::max(0, std::min(16, api_knob("STENCIL_SLAB_XCU", 0))); }
+    static int stream_create(Stream* s, int role) {
+        const int c = xcu();
+        const bool excl = c > 0 && api_knob("STENCIL_SLAB_XCU_EXCL", 0) != 0;
+        if (role == slab::STREAM_EXCHANGE ? c > 0 : excl) {
+            int dev = 0, cus = 0;
+            STENCIL_HIP_CHECK(hipGetDevice(&dev));
+            STENCIL_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            // CU-mask bit b selects CU b / nxcd of XCD b % nxcd (the driver
+            // stripes a queue's mask over the XCDs): bits [0, c * 8) are c CUs
+            // on each of the 8 XCDs
+            constexpr int kXcds = 8;
+            std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0u);
+            for (int b = 0; b < cus; ++b) {
+                const bool xbit = b < c * kXcds;
+                if (xbit == (role == slab::STREAM_EXCHANGE)) mask[size_t(b / 32)] |= 1u << (b % 32);
+            }
+            if (hipExtStreamCreateWithCUMask(s, uint32_t(mask.size()), mask.data()) != hipSuccess)
+                return set_error(STENCIL_EHIP, "CU-masked stream creation failed");
+            return STENCIL_OK;
+        }
         int lo_prio = 0, hi_prio = 0;
-        // STENCIL_SLAB_NOPRIO=1 (debug library): both streams at the default priority
+        bool high_priority = role != slab::STREAM_INTERIOR;
+        // STENCIL_SLAB_NOPRIO=1 (debug library): every stream at the default priority
         if (knob("STENCIL_SLAB_NOPRIO", 0)) high_priority = false;
         if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess ||
             hipStreamCreateWithPriority(s, hipStreamNonBlocking, high_priority ? hi_prio : lo_prio) != hipSuccess)
@@ -166,6 +233,37 @@ struct HipDev {
     static int stream_sync(Stream s) {
         STENCIL_HIP_CHECK(hipStreamSynchronize(s));
         return STENCIL_OK;
+    }
+    // Bounded waits: poll the stream / event, and the communicator's
+    // asynchronous error, until done or past the deadline (then
+    // STENCIL_ETIMEOUT; the caller fails the job).  Spins with a yield: the
+    // end of a timed run() waits here.
+    static int default_timeout_ms() { return std::max(1, api_knob("STENCIL_SLAB_TIMEOUT_MS", 60000)); }
+    template <class Q>
+    static int poll_until(Q&& query, Comm c, slab::Clock::time_point deadline, const char* what) {
+        for (uint64_t it = 0;; ++it) {
+            const hipError_t e = query();
+            if (e == hipSuccess) return STENCIL_OK;
+            if (e != hipErrorNotReady) return set_error(STENCIL_EHIP, "%s: %s", what, hipGetErrorString(e));
+            if ((it & 63) == 63) {
+                if (c && rccl().ok) {
+                    ncclResult_t r = ncclSuccess;
+                    if (rccl().CommGetAsyncError(c, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
+                        return set_error(STENCIL_EHIP, "%s: RCCL asynchronous error: %s", what, rccl().GetErrorString(r));
+                }
+                if (slab::Clock::now() > deadline)
+                    return set_error(STENCIL_ETIMEOUT, "%s: no progress before the slab job's deadline (a peer stopped "
+                                     "answering?): the job is failed and its communicators aborted", what);
+            }
+            if (it > 4096) std::this_thread::sleep_for(std::chrono::microseconds(20));
+            else std::this_thread::yield();
+        }
+    }
+    static int sync_until(Stream s, Comm c, slab::Clock::time_point deadline) {
+        return poll_until([&] { return hipStreamQuery(s); }, c, deadline, "slab stream");
+    }
+    static int event_sync_until(Event e, Comm c, slab::Clock::time_point deadline) {
+        return poll_until([&] { return hipEventQuery(e); }, c, deadline, "slab round");
     }
     static int event_create(Event* e, bool timing) {
         STENCIL_HIP_CHECK(timing ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -207,13 +305,11 @@ struct HipDev {
     }
     static void face_signal_destroy(uint64_t* fs) { (void)stencil_face_signal_destroy(fs); }
     static int wait_face_signal(uint64_t* fs, uint64_t target, Stream s) { return stencil_wait_face_signal(fs, target, s); }
-    static int wait_counters(uint32_t* c, uint32_t lo, uint32_t hi, Stream s) {
-        return stencil_wait_counters(c, lo, hi, c + 2, s);
+    static int wait_counters(uint32_t* c, uint32_t* flag, uint32_t lo, uint32_t hi, Stream s) {
+        return stencil_wait_counters(c, lo, hi, flag, s);
     }
-    static int read_timeout(uint32_t* c, bool* timed_out) {
-        uint32_t flag = 0;
-        STENCIL_HIP_CHECK(hipMemcpy(&flag, c + 2, sizeof(flag), hipMemcpyDeviceToHost));
-        *timed_out = flag != 0;
+    static int read_timeout(uint32_t* flag, bool* timed_out) {
+        *timed_out = __atomic_load_n(flag, __ATOMIC_SEQ_CST) != 0;
         return STENCIL_OK;
     }
     static int copy_d2d(void* dst, const void* src, size_t bytes, Stream s) {
@@ -254,6 +350,11 @@ struct HipDev {
     static void comm_destroy(Comm c) {
         if (rccl().ok) (void)rccl().CommDestroy(c);
     }
+    // abort: RCCL's kernels still waiting for a peer return (and the comm is freed)
+    static void comm_abort(Comm c) {
+        if (rccl().ok) (void)rccl().CommAbort(c);
+    }
+    static void comm_set_timeout(Comm, int64_t) {}  // the bound is enforced by the polling waits
     static int group_start() {
         SLAB_NCCL_CHECK(rccl().GroupStart());
         return STENCIL_OK;
@@ -358,6 +459,14 @@ int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* la
 
 int stencil_slab_plane_sums(stencil_slab_job* job, double* sums) {
     return core::plane_sums<HipDev>(job, sums);
+}
+
+int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form) {
+    return core::round_form<HipDev>(job, form);
+}
+
+int stencil_slab_set_timeout(stencil_slab_job* job, int64_t timeout_ms) {
+    return core::set_timeout<HipDev>(job, timeout_ms);
 }
 
 }  // extern "C"

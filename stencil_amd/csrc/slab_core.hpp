@@ -61,18 +61,32 @@ struct Slab {
     // two grids a / b; rolling: `a` is the one allocation (margin + grid), b null
     void* a = nullptr;
     void* b = nullptr;
-    typename Dev::Stream sa{}, sb{};  // boundary + exchange (high priority) / interior
-    typename Dev::Event ev_bnd{}, ev_int{}, ev_join{};
+    typename Dev::Stream sa{}, sb{};  // boundary launches (high priority) / interior
+    // the exchange: its own queue, which HipDev may confine to a few CUs per
+    // XCD (STENCIL_SLAB_XCU), bracketed by events so that A sees it in order
+    typename Dev::Stream sx{};
+    typename Dev::Event ev_bnd{}, ev_int{}, ev_join{}, ev_xin{}, ev_xout{};
+    // the last kInflight rounds' exchange completions: run() keeps at most
+    // that many rounds queued and waits for them with the job's deadline
+    std::vector<typename Dev::Event> ring;
     typename Dev::Comm comm{};
     // face-signalled rounds: [0] low-face adds, [1] high-face adds (they run
-    // on across launches), [2] the wait kernel's timeout flag
+    // on across launches); tflag: the wait kernel's timeout flag (host-
+    // coherent on HIP: the host releases a queued wait by setting it)
     uint32_t* counters = nullptr;
+    uint32_t* tflag = nullptr;
     uint32_t sig_target = 0;  // adds per face expected once the last queued launch is done
     // STENCIL_SLAB_CPWAIT: the launch also adds 1 per completed face to this
     // HIP signal word, and the exchange stream waits on it in the command
     // processor (hipStreamWaitValue64) instead of a polling wait kernel
     uint64_t* fsig = nullptr;
     uint64_t fsig_target = 0;
+    // overlapped rolling rounds: the new grid's faces are computed into the
+    // send staging xs and travel from there while the pass runs; the
+    // neighbours' faces land in the receive staging xr and are copied into
+    // the halo slots after the pass (2 x depth planes each: lo face, hi face)
+    void* xs = nullptr;
+    void* xr = nullptr;
 };
 
 template <class Dev>
@@ -92,13 +106,29 @@ struct Job {
     // shifted to the allocation's start
     int64_t margin = 0;
     int position = 0;
+    bool roll_overlap = false;  // rolling rounds with the exchange beside the pass (staged faces)
     std::vector<Slab<Dev>> s;
     // kernel timing: events around slab 0's compute launch(es) of every round
     bool timing = false;
     std::vector<std::pair<typename Dev::Event, typename Dev::Event>> tev;
     int64_t timed_cells = 0;
     int64_t timed_launches = 0;  // kernel launches inside the timed spans
+    // bounded-time failure: every wait for the devices gives up after
+    // timeout_ms (a peer that stopped posting leaves RCCL's receive spinning);
+    // the job then aborts its communicators and every later call fails with
+    // `failed` (destroy is the only thing left to do)
+    int64_t timeout_ms = 60000;
+    int failed = STENCIL_OK;
+    uint64_t rounds = 0;  // rounds issued (the in-flight ring's index)
 };
+
+constexpr int kInflight = 8;  // rounds queued ahead of the last completed exchange
+
+// the roles of a slab's streams (Dev::stream_create): boundary launches (high
+// priority), the interior / whole-slab launches, the halo exchange
+enum StreamRole { STREAM_BOUNDARY = 0, STREAM_INTERIOR = 1, STREAM_EXCHANGE = 2 };
+
+using Clock = std::chrono::steady_clock;
 
 #define SLAB_TRY(expr)               \
     do {                             \
@@ -173,12 +203,30 @@ void drop_timing(Job<Dev>& j) {
 // ---- exchange -------------------------------------------------------------
 // Halo exchange of the grids at rolling position `pos` (each slab's copy of
 // the same logical grid): every slab's `depth` face planes into its
-// neighbours' halo planes, queued on the slabs' A streams behind what is
-// already there.  Faces are contiguous whole planes: nothing is packed.
-template <class Dev>
-int exchange(Job<Dev>& j, int pos) {
+// neighbours' halo planes.  Faces are contiguous whole planes: nothing is
+// packed.  The transfers run on each slab's exchange stream X, bracketed so
+// that they behave as if queued on A behind what is already there: X first
+// waits for A (ev_xin), then `pre(slab)` queues what must precede the
+// transfers on X (a face-signalled round's wait for its faces), and A finally
+// waits for X (ev_xout).  On HIP, X is a queue of its own, which may be
+// confined to a few CUs per XCD so that RCCL's or the copies' kernels do not
+// take the CUs a one-per-CU launch beside them counts on.
+struct NoPre {
+    template <class S>
+    int operator()(S&) const { return STENCIL_OK; }
+};
+
+template <class Dev, class Pre = NoPre>
+int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
     const int n = int(j.s.size());
     const int64_t d = j.depth;
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ev_xin, s.sa));
+        SLAB_TRY(Dev::stream_wait(s.sx, s.ev_xin));
+        SLAB_TRY(pre(s));
+        SLAB_TRY(Dev::event_record(s.ev_join, s.sx));  // this slab's faces are ready
+    }
     if (j.exchange == STENCIL_EXCHANGE_RCCL) {
         SLAB_TRY(Dev::group_start());
         int rc = STENCIL_OK;
@@ -190,71 +238,57 @@ int exchange(Job<Dev>& j, int pos) {
             // sends and receives to one peer match in posting order: a slab
             // that is its own neighbour (periodic, N = 1) sends hi -> recv lo
             // first, then lo -> hi
-            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, s.n - d), bytes, hi, s.comm, s.sa);
-            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, -d), bytes, lo, s.comm, s.sa);
-            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, 0), bytes, lo, s.comm, s.sa);
-            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, s.n), bytes, hi, s.comm, s.sa);
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, s.n - d), bytes, hi, s.comm, s.sx);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, -d), bytes, lo, s.comm, s.sx);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::send(plane_ptr(s, g, 0), bytes, lo, s.comm, s.sx);
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::recv(plane_ptr(s, g, s.n), bytes, hi, s.comm, s.sx);
         }
         const int rc2 = Dev::group_end();
-        return rc != STENCIL_OK ? rc : rc2;
+        SLAB_TRY(rc != STENCIL_OK ? rc : rc2);
+    } else {
+        // device copies (single-process jobs only: local = global index):
+        // slab i's X pulls its neighbours' faces once they are ready (ev_join)
+        for (int i = 0; i < n; ++i) {
+            Slab<Dev>& s = j.s[size_t(i)];
+            SLAB_TRY(Dev::set_device(s.device));
+            void* g = grid_at(j, s, pos);
+            const size_t bytes = size_t(d) * plane_bytes(s);
+            const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+            SLAB_TRY(Dev::debug_delay(s.sx, i));  // tests: slab 0's pulls slow (a no-op unless asked for)
+            if (lo >= 0) {
+                Slab<Dev>& t = j.s[size_t(lo)];
+                SLAB_TRY(Dev::stream_wait(s.sx, t.ev_join));
+                SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, -d), s.device, plane_ptr(t, grid_at(j, t, pos), t.n - d),
+                                        t.device, bytes, s.sx));
+            }
+            if (hi >= 0) {
+                Slab<Dev>& t = j.s[size_t(hi)];
+                SLAB_TRY(Dev::stream_wait(s.sx, t.ev_join));
+                SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, s.n), s.device, plane_ptr(t, grid_at(j, t, pos), 0), t.device,
+                                        bytes, s.sx));
+            }
+        }
     }
-    // device copies (single-process jobs only: local = global index): slab i's
-    // A stream pulls its neighbours' faces once their round is complete
-    // (ev_join, recorded on their A streams after joining B)
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
-        SLAB_TRY(Dev::event_record(s.ev_join, s.sa));
+        SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
     }
     for (int i = 0; i < n; ++i) {
         Slab<Dev>& s = j.s[size_t(i)];
         SLAB_TRY(Dev::set_device(s.device));
-        void* g = grid_at(j, s, pos);
-        const size_t bytes = size_t(d) * plane_bytes(s);
-        const int lo = lo_nb(j, i), hi = hi_nb(j, i);
-        SLAB_TRY(Dev::debug_delay(s.sa, i));  // tests: slab 0's pulls slow (a no-op unless asked for)
-        if (lo >= 0) {
-            Slab<Dev>& t = j.s[size_t(lo)];
-            SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
-            SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, -d), s.device, plane_ptr(t, grid_at(j, t, pos), t.n - d), t.device,
-                                    bytes, s.sa));
-        }
-        if (hi >= 0) {
-            Slab<Dev>& t = j.s[size_t(hi)];
-            SLAB_TRY(Dev::stream_wait(s.sa, t.ev_join));
-            SLAB_TRY(Dev::copy_peer(plane_ptr(s, g, s.n), s.device, plane_ptr(t, grid_at(j, t, pos), 0), t.device, bytes,
-                                    s.sa));
-        }
-    }
-    if (j.margin && Dev::pull_wait_enabled()) {
-        // Rolling slabs: a slab's next pass writes its new grid over the
-        // planes its neighbours are still pulling faces from (the grid moves
-        // by the shift every round), so every slab waits for its neighbours'
-        // pulls first.  Two-grid jobs need no such wait: the next round
-        // writes the other grid, and the round after waits on this one.
-        // (RCCL exchanges are ordered by each slab's own stream.)
-        for (Slab<Dev>& s : j.s) {
-            SLAB_TRY(Dev::set_device(s.device));
-            SLAB_TRY(Dev::event_record(s.ev_join, s.sa));
-        }
-        for (int i = 0; i < n; ++i) {
-            Slab<Dev>& s = j.s[size_t(i)];
-            SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::stream_wait(s.sa, s.ev_xout));
+        if (j.margin && j.exchange == STENCIL_EXCHANGE_COPY && Dev::pull_wait_enabled()) {
+            // Rolling slabs: a slab's next pass writes its new grid over the
+            // planes its neighbours are still pulling faces from (the grid
+            // moves by the shift every round), so every slab waits for its
+            // neighbours' pulls first.  Two-grid jobs need no such wait: the
+            // next round writes the other grid, and the round after waits on
+            // this one.  (RCCL exchanges are ordered by each slab's own X.)
             const int lo = lo_nb(j, i), hi = hi_nb(j, i);
-            if (lo >= 0 && lo != i) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(lo)].ev_join));
-            if (hi >= 0 && hi != i && hi != lo) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(hi)].ev_join));
+            if (lo >= 0 && lo != i) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(lo)].ev_xout));
+            if (hi >= 0 && hi != i && hi != lo) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(hi)].ev_xout));
         }
     }
-    return STENCIL_OK;
-}
-
-template <class Dev>
-int sync_all(Job<Dev>& j) {
-    for (Slab<Dev>& s : j.s) {
-        SLAB_TRY(Dev::set_device(s.device));
-        SLAB_TRY(Dev::stream_sync(s.sa));
-        SLAB_TRY(Dev::stream_sync(s.sb));
-    }
-    j.chained = false;
     return STENCIL_OK;
 }
 
@@ -331,14 +365,13 @@ int slab_round_signal(Job<Dev>& j, int k) {
         SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, 1));
         SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
         s.sig_target += uint32_t(nsig);
-        if (s.fsig) {  // both faces of this launch: +2
-            s.fsig_target += 2;
-            SLAB_TRY(Dev::wait_face_signal(s.fsig, s.fsig_target, s.sa));
-        } else {
-            SLAB_TRY(Dev::wait_counters(s.counters, s.sig_target, s.sig_target, s.sa));
-        }
+        if (s.fsig) s.fsig_target += 2;  // both faces of this launch: +2
     }
-    SLAB_TRY(exchange(j, dst_pos));
+    // the wait for the faces goes first on the exchange stream
+    SLAB_TRY(exchange(j, dst_pos, [](Slab<Dev>& s) {
+        return s.fsig ? Dev::wait_face_signal(s.fsig, s.fsig_target, s.sx)
+                      : Dev::wait_counters(s.counters, s.tflag, s.sig_target, s.sig_target, s.sx);
+    }));
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
         SLAB_TRY(Dev::event_record(s.ev_bnd, s.sa));
@@ -397,6 +430,130 @@ int slab_round_rolling(Job<Dev>& j, int k) {
     return STENCIL_OK;
 }
 
+// The overlapped rolling round (the default for rolling slabs with a shared
+// face; STENCIL_SLAB_ROLLING_OVERLAP=0 runs the serial form above).  In the
+// serial form the exchange must wait for the whole pass: the new grid's late
+// face is written by the pass's last launch, and the halo slots it receives
+// into are home-grid planes the last launches still read.  Here, per slab:
+//   1. on A, the new grid's faces [0, d) and [n - d, n) are computed first,
+//      from the old grid (whole before the pass), into the send staging xs:
+//      one stencil_sweepk of d planes each, the same kernels and sums as the
+//      pass, so the bits are those the pass writes into the grid;
+//   2. on X, the exchange from xs into the neighbours' receive staging xr,
+//      as soon as those launches are done -- beside the pass;
+//   3. on A, the pass (unchanged, it still writes the face planes);
+//   4. on A, after the pass and the exchange, xr into the new grid's halo
+//      slots (d planes per shared face), and the global ends' ghost restores.
+// The reference overlaps the same way: halo DMA issued before the interior
+// rows and waited for after them (stencil_dma.cpp:426, 448), edge results
+// put as each edge is computed (stencil_dma.cpp:475-559).
+template <class Dev>
+inline void* staged_grid(const Slab<Dev>& s, void* buf, int64_t b) {
+    // the base whose plane b is buf's first plane (sweepk writes only [b, e))
+    return static_cast<char*>(buf) - size_t(s.l.zghost + b) * plane_bytes(s);
+}
+
+template <class Dev>
+int slab_round_rolling_overlap(Job<Dev>& j, int k) {
+    const int64_t S = rolling_span(j);
+    const int64_t d = j.depth;
+    const bool down = j.position == 0;
+    const int src_pos = j.position, dst_pos = 1 - j.position;
+    const int n = int(j.s.size());
+    // 1. the faces into the send staging
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        const size_t pb = plane_bytes(s);
+        SLAB_TRY(time_begin(j, i, s.sa));  // the timed span: the face launches and the pass
+        if (lo_nb(j, s.index) >= 0) SLAB_TRY(Dev::sweepk(&s.l, src, staged_grid(s, s.xs, 0), 0, d, k, s.sa));
+        if (hi_nb(j, s.index) >= 0)
+            SLAB_TRY(Dev::sweepk(&s.l, src, staged_grid(s, static_cast<char*>(s.xs) + size_t(d) * pb, s.n - d), s.n - d,
+                                 s.n, k, s.sa));
+        SLAB_TRY(Dev::event_record(s.ev_join, s.sa));  // this slab's faces are staged
+    }
+    // 2. the exchange on X, from the staging, beside the pass
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::stream_wait(s.sx, s.ev_join));
+    }
+    if (j.exchange == STENCIL_EXCHANGE_RCCL) {
+        SLAB_TRY(Dev::group_start());
+        int rc = STENCIL_OK;
+        for (int i = 0; i < n && rc == STENCIL_OK; ++i) {
+            Slab<Dev>& s = j.s[size_t(i)];
+            const size_t pb = plane_bytes(s), bytes = size_t(d) * pb;
+            char* xs = static_cast<char*>(s.xs);
+            char* xr = static_cast<char*>(s.xr);
+            const int lo = lo_nb(j, s.index), hi = hi_nb(j, s.index);
+            // the posting order of exchange(): a slab that is its own
+            // neighbour sends hi -> receives lo first
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::send(xs + bytes, bytes, hi, s.comm, s.sx);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::recv(xr, bytes, lo, s.comm, s.sx);
+            if (lo >= 0 && rc == STENCIL_OK) rc = Dev::send(xs, bytes, lo, s.comm, s.sx);
+            if (hi >= 0 && rc == STENCIL_OK) rc = Dev::recv(xr + bytes, bytes, hi, s.comm, s.sx);
+        }
+        const int rc2 = Dev::group_end();
+        SLAB_TRY(rc != STENCIL_OK ? rc : rc2);
+    } else {
+        for (int i = 0; i < n; ++i) {
+            Slab<Dev>& s = j.s[size_t(i)];
+            SLAB_TRY(Dev::set_device(s.device));
+            const size_t bytes = size_t(d) * plane_bytes(s);
+            const int lo = lo_nb(j, i), hi = hi_nb(j, i);
+            SLAB_TRY(Dev::debug_delay(s.sx, i));
+            if (lo >= 0) {  // the low neighbour's high face
+                Slab<Dev>& t = j.s[size_t(lo)];
+                SLAB_TRY(Dev::stream_wait(s.sx, t.ev_join));
+                SLAB_TRY(Dev::copy_peer(s.xr, s.device, static_cast<char*>(t.xs) + bytes, t.device, bytes, s.sx));
+            }
+            if (hi >= 0) {  // the high neighbour's low face
+                Slab<Dev>& t = j.s[size_t(hi)];
+                SLAB_TRY(Dev::stream_wait(s.sx, t.ev_join));
+                SLAB_TRY(Dev::copy_peer(static_cast<char*>(s.xr) + bytes, s.device, t.xs, t.device, bytes, s.sx));
+            }
+        }
+    }
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
+    }
+    // 3. the pass, 4. the halos out of the staging
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        void* dst = grid_at(j, s, dst_pos);
+        const int64_t J = (s.n + S - 1) / S;
+        for (int64_t q = 0; q < J; ++q) {
+            const int64_t jj = down ? q : J - 1 - q;
+            const int64_t b = jj * S, e = std::min(s.n, b + S);
+            SLAB_TRY(Dev::sweepk(&s.l, src, dst, b, e, k, s.sa));
+        }
+        const int64_t lo = lo_nb(j, int(s.index)), hi = hi_nb(j, int(s.index));
+        SLAB_TRY(time_end(j, i, s.sa, s.l.prob.nx * s.l.prob.ny * s.n, J + (lo >= 0) + (hi >= 0)));
+        const int64_t zg = s.l.zghost;
+        const size_t pb = plane_bytes(s), bytes = size_t(d) * pb;
+        if (down && hi < 0)  // the shifted grid's top ghosts from the home grid's (never written)
+            SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, s.n), plane_ptr(s, src, s.n), size_t(zg) * pb, s.sa));
+        if (!down && lo < 0)  // the home grid's bottom ghosts from the shifted grid's (never written)
+            SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, -zg), plane_ptr(s, src, -zg), size_t(zg) * pb, s.sa));
+        SLAB_TRY(Dev::stream_wait(s.sa, s.ev_xout));
+        if (lo >= 0) SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, -d), s.xr, bytes, s.sa));
+        if (hi >= 0) SLAB_TRY(Dev::copy_d2d(plane_ptr(s, dst, s.n), static_cast<char*>(s.xr) + bytes, bytes, s.sa));
+        if (j.exchange == STENCIL_EXCHANGE_COPY && Dev::pull_wait_enabled()) {
+            // the neighbours pulled from this slab's xs, which the next
+            // round's face launches overwrite
+            if (lo >= 0 && lo != int64_t(i)) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(lo)].ev_xout));
+            if (hi >= 0 && hi != int64_t(i) && hi != lo) SLAB_TRY(Dev::stream_wait(s.sa, j.s[size_t(hi)].ev_xout));
+        }
+    }
+    j.position = dst_pos;
+    j.chained = false;
+    return STENCIL_OK;
+}
+
 // Did a face-counter wait give up?  Then the halos are wrong.
 template <class Dev>
 int check_signal_timeouts(Job<Dev>& j) {
@@ -404,9 +561,74 @@ int check_signal_timeouts(Job<Dev>& j) {
         if (!s.counters) continue;
         SLAB_TRY(Dev::set_device(s.device));
         bool timed_out = false;
-        SLAB_TRY(Dev::read_timeout(s.counters, &timed_out));
-        if (timed_out) return set_error(STENCIL_EHIP, "slab on device %d: a face-counter wait timed out", s.device);
+        SLAB_TRY(Dev::read_timeout(s.tflag, &timed_out));
+        if (timed_out) return set_error(STENCIL_ETIMEOUT, "slab on device %d: a face-counter wait timed out", s.device);
     }
+    return STENCIL_OK;
+}
+
+// ---- bounded-time failure ---------------------------------------------------
+// A failure the job cannot recover from (a device wait past the deadline, an
+// asynchronous RCCL error, a failed launch): abort the communicators (RCCL's
+// kernels waiting for a peer that stopped posting then return), release any
+// face-signal or face-counter wait still queued, and make every later call
+// fail.  Keeps the message of the error that caused it.
+template <class Dev>
+int fail(Job<Dev>& j, int rc) {
+    if (rc == STENCIL_OK || j.failed) return rc;
+    j.failed = rc;
+    for (Slab<Dev>& s : j.s) {
+        (void)Dev::set_device(s.device);
+        if (s.comm) {
+            Dev::comm_abort(s.comm);
+            s.comm = typename Dev::Comm{};
+        }
+        Dev::release_waits(s.tflag, s.fsig);
+    }
+    return rc;
+}
+
+template <class Dev>
+int check_alive(const Job<Dev>& j) {
+    if (!j.failed) return STENCIL_OK;
+    return set_error(j.failed, "the slab job failed earlier (its communicators were aborted): destroy it");
+}
+
+// Wait for everything queued on every slab's streams, at most until the job's
+// deadline; a failure fails the job.
+template <class Dev>
+int sync_bounded(Job<Dev>& j) {
+    SLAB_TRY(check_alive(j));
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(j.timeout_ms);
+    for (Slab<Dev>& s : j.s) {
+        if (int rc = Dev::set_device(s.device)) return fail(j, rc);
+        for (typename Dev::Stream st : {s.sx, s.sa, s.sb})
+            if (int rc = Dev::sync_until(st, s.comm, deadline)) return fail(j, rc);
+    }
+    j.chained = false;
+    return STENCIL_OK;
+}
+
+// Before issuing a round: at most kInflight rounds may be queued behind the
+// last exchange known complete (this bounds the queues, and a peer that
+// stopped posting is noticed while rounds are issued, not only at the end).
+template <class Dev>
+int throttle(Job<Dev>& j) {
+    if (j.rounds < uint64_t(kInflight)) return STENCIL_OK;
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(j.timeout_ms);
+    for (Slab<Dev>& s : j.s) {
+        if (int rc = Dev::set_device(s.device)) return fail(j, rc);
+        if (int rc = Dev::event_sync_until(s.ring[size_t(j.rounds % kInflight)], s.comm, deadline)) return fail(j, rc);
+    }
+    return STENCIL_OK;
+}
+template <class Dev>
+int mark_round(Job<Dev>& j) {
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::event_record(s.ring[size_t(j.rounds % kInflight)], s.sx));
+    }
+    ++j.rounds;
     return STENCIL_OK;
 }
 
@@ -418,19 +640,38 @@ void release(JobT* j) {
         (void)Dev::set_device(j->s[0].device);
         drop_timing(*j);
     }
+    // drain the queues within the job's deadline; if they do not drain, fail
+    // the job (abort the communicators, release the waits) and try once more;
+    // memory still in use then is leaked rather than freed under a kernel
+    auto drain = [&]() {
+        bool ok = true;
+        const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(j->timeout_ms);
+        for (Slab<Dev>& s : j->s) {
+            (void)Dev::set_device(s.device);
+            for (typename Dev::Stream st : {s.sx, s.sa, s.sb})
+                if (st) ok = Dev::sync_until(st, s.comm, deadline) == STENCIL_OK && ok;
+        }
+        return ok;
+    };
+    bool drained = drain();
+    if (!drained) {
+        (void)fail(*j, STENCIL_ETIMEOUT);
+        drained = drain();
+    }
     for (Slab<Dev>& s : j->s) {
         (void)Dev::set_device(s.device);
-        if (s.sa) (void)Dev::stream_sync(s.sa);
-        if (s.sb) (void)Dev::stream_sync(s.sb);
         if (s.comm) Dev::comm_destroy(s.comm);
-        if (s.a) Dev::free(s.a);
-        if (s.b) Dev::free(s.b);
-        if (s.sa) Dev::stream_destroy(s.sa);
-        if (s.sb) Dev::stream_destroy(s.sb);
-        if (s.ev_bnd) Dev::event_destroy(s.ev_bnd);
-        if (s.ev_int) Dev::event_destroy(s.ev_int);
-        if (s.ev_join) Dev::event_destroy(s.ev_join);
+        if (!drained) continue;
+        for (void* p : {s.a, s.b, s.xs, s.xr})
+            if (p) Dev::free(p);
+        for (typename Dev::Stream st : {s.sx, s.sa, s.sb})
+            if (st) Dev::stream_destroy(st);
+        for (typename Dev::Event e : {s.ev_bnd, s.ev_int, s.ev_join, s.ev_xin, s.ev_xout})
+            if (e) Dev::event_destroy(e);
+        for (typename Dev::Event e : s.ring)
+            if (e) Dev::event_destroy(e);
         if (s.counters) Dev::free_counters(s.counters);
+        if (s.tflag) Dev::free_flag(s.tflag);
         if (s.fsig) Dev::face_signal_destroy(s.fsig);
     }
     delete j;
@@ -493,6 +734,7 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct && !rolling &&
                     !j->serial && Dev::signal_enabled();
     }
+    j->timeout_ms = Dev::default_timeout_ms();
     const int64_t base = g.nz / total, rem = g.nz % total;
     // the smallest slab of the job decides, the same in every process: ranks
     // of one job all reject it here, before any of them enters the
@@ -520,6 +762,13 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         if ((rc = Dev::layout_init(&p, &s.l))) break;
         if ((rc = Dev::set_device(s.device))) break;
         if (rolling) {
+            // the overlapped rounds' face staging first (2 x d planes to send,
+            // 2 x d to receive), then the margin from what memory is left
+            j->roll_overlap = Dev::rolling_overlap() && (total > 1 || j->periodic);
+            if (j->roll_overlap) {
+                const int64_t sb = 2 * int64_t(j->depth) * int64_t(plane_bytes(s));
+                if ((rc = Dev::alloc(sb, &s.xs)) || (rc = Dev::alloc(sb, &s.xr))) break;
+            }
             int64_t m = 0;
             if ((rc = rolling_margin(*j, s.l, margin, &m))) break;
             // one margin for the job (the largest slab decides when sized from free memory)
@@ -529,11 +778,16 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         } else {
             if ((rc = Dev::alloc(s.l.bytes + 256, &s.a)) || (rc = Dev::alloc(s.l.bytes + 256, &s.b))) break;
         }
-        if ((rc = Dev::stream_create(&s.sa, true)) || (rc = Dev::stream_create(&s.sb, false)) ||
-            (rc = Dev::event_create(&s.ev_bnd, false)) || (rc = Dev::event_create(&s.ev_int, false)) ||
-            (rc = Dev::event_create(&s.ev_join, false)))
+        if ((rc = Dev::stream_create(&s.sa, STREAM_BOUNDARY)) || (rc = Dev::stream_create(&s.sb, STREAM_INTERIOR)) ||
+            (rc = Dev::stream_create(&s.sx, STREAM_EXCHANGE)) || (rc = Dev::event_create(&s.ev_bnd, false)) ||
+            (rc = Dev::event_create(&s.ev_int, false)) || (rc = Dev::event_create(&s.ev_join, false)) ||
+            (rc = Dev::event_create(&s.ev_xin, false)) || (rc = Dev::event_create(&s.ev_xout, false)))
             break;
-        if ((rc = Dev::alloc_counters(&s.counters))) break;
+        s.ring.assign(size_t(kInflight), typename Dev::Event{});
+        for (auto& e : s.ring)
+            if ((rc = Dev::event_create(&e, false))) break;
+        if (rc) break;
+        if ((rc = Dev::alloc_counters(&s.counters)) || (rc = Dev::alloc_flag(&s.tflag))) break;
         if (j->signal && (rc = Dev::face_signal_create(&s.fsig))) break;
     }
     if (rc != STENCIL_OK) {
@@ -585,7 +839,10 @@ int create(const stencil_problem* global, int32_t ngpus, const int32_t* devices,
             release<Dev>(j);
             return rc;
         }
-        for (int i = 0; i < ngpus; ++i) j->s[size_t(i)].comm = comms[size_t(i)];
+        for (int i = 0; i < ngpus; ++i) {
+            j->s[size_t(i)].comm = comms[size_t(i)];
+            Dev::comm_set_timeout(comms[size_t(i)], j->timeout_ms);
+        }
     }
     *job = j;
     clear_error();
@@ -618,6 +875,7 @@ int create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int
         return rc;
     }
     j->s[0].comm = comm;
+    Dev::comm_set_timeout(comm, j->timeout_ms);
     *job = j;
     clear_error();
     return STENCIL_OK;
@@ -660,29 +918,83 @@ int init_margin(const Job<Dev>& j, Slab<Dev>& s) {
     const size_t pb = plane_bytes(s);
     for (int64_t i = 0; i < j.margin; ++i)
         SLAB_TRY(Dev::copy_d2d(static_cast<char*>(s.a) + size_t(i) * pb, plane_ptr(s, home, -1), pb, s.sa));
+    // the face staging's planes likewise: the face launches write only the
+    // interior, the x/y ghost ring they send is this copy's
+    for (void* buf : {s.xs, s.xr})
+        if (buf)
+            for (int64_t i = 0; i < 2 * j.depth; ++i)
+                SLAB_TRY(Dev::copy_d2d(static_cast<char*>(buf) + size_t(i) * pb, plane_ptr(s, home, -1), pb, s.sa));
     return STENCIL_OK;
 }
+
+// Counters and face signals back to zero (a job whose face-counter wait
+// timed out earlier starts clean: the timeout flag is sticky otherwise).
+template <class Dev>
+int reset_signals(Job<Dev>& j) {
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(Dev::reset_counters(s.counters, s.tflag, s.fsig));
+        s.sig_target = 0;
+        s.fsig_target = 0;
+    }
+    return STENCIL_OK;
+}
+
+#define SLAB_FAIL(j, expr)                       \
+    do {                                         \
+        if (int rc_ = (expr)) return fail(j, rc_); \
+    } while (0)
 
 template <class Dev, class JobT>
 int fill_initial(JobT* job, int32_t init_kind, uint64_t seed) {
     if (!job) return set_error(STENCIL_EINVAL, "null job");
-    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(sync_bounded(*job));
+    SLAB_FAIL(*job, reset_signals(*job));
     job->cur_is_a = true;
     job->position = 0;
     for (Slab<Dev>& s : job->s) {
-        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_FAIL(*job, Dev::set_device(s.device));
         // global linear indices: the slab's interior starts first * nx * ny cells in
         const uint64_t sd = seed + uint64_t(s.first) * uint64_t(s.l.prob.nx) * uint64_t(s.l.prob.ny);
-        SLAB_TRY(Dev::fill_initial(&s.l, grid_at(*job, s, 0), init_kind, sd, s.sa));
+        SLAB_FAIL(*job, Dev::fill_initial(&s.l, grid_at(*job, s, 0), init_kind, sd, s.sa));
         if (job->margin)
-            SLAB_TRY(init_margin(*job, s));
+            SLAB_FAIL(*job, init_margin(*job, s));
         else
-            SLAB_TRY(Dev::fill_initial(&s.l, s.b, init_kind, sd, s.sa));
+            SLAB_FAIL(*job, Dev::fill_initial(&s.l, s.b, init_kind, sd, s.sa));
     }
     // the halos: the neighbours' faces (ghost planes otherwise)
-    SLAB_TRY(exchange(*job, 0));
-    if (!job->margin) SLAB_TRY(exchange(*job, 1));
-    return sync_all(*job);
+    SLAB_FAIL(*job, exchange(*job, 0));
+    if (!job->margin) SLAB_FAIL(*job, exchange(*job, 1));
+    SLAB_TRY(sync_bounded(*job));
+    clear_error();
+    return STENCIL_OK;
+}
+
+// Rolling slabs need every plane's x/y ghost ring to be the same and the
+// bottom ghost planes to be equal: no sweep writes a
+// ghost cell, and a pass lands plane z of the new grid in a slot whose ring
+// came from an older plane or from the margin's copies of plane -1.  The
+// reference initial condition has this; an uploaded grid must too.
+template <class T>
+int check_rolling_rings(const T* h, const stencil_problem& g, int64_t row, int64_t rows) {
+    const int64_t r = g.radius, w = g.nx + 2 * r, hgt = g.ny + 2 * r, planes = g.nz + 2 * r;
+    const size_t hp = size_t(row) * size_t(rows);
+    auto ring_cell = [&](int64_t y, int64_t x) { return y < r || y >= g.ny + r || x < r || x >= g.nx + r; };
+    for (int64_t z = 1; z < planes; ++z)
+        for (int64_t y = 0; y < hgt; ++y)
+            for (int64_t x = 0; x < w; ++x) {
+                if (!ring_cell(y, x) && !(z < r)) continue;  // bottom ghost planes: every cell
+                const T a = h[size_t(z) * hp + size_t(y * row + x)];
+                const T b = h[(z < r ? size_t(r - 1) * hp : 0) + size_t(y * row + x)];
+                if (std::memcmp(&a, &b, sizeof(T)) != 0)
+                    return set_error(STENCIL_EINVAL,
+                                     "rolling slab upload: host plane %lld cell (x %lld, y %lld) differs from %s -- "
+                                     "rolling slabs need the same x/y ghost ring in every plane and equal bottom "
+                                     "ghost planes (use two grids: no STENCIL_SLAB_ROLLING)",
+                                     (long long)(z - r), (long long)(x - r), (long long)(y - r),
+                                     z < r ? "ghost plane -1" : "the ring of ghost plane -r");
+            }
+    return STENCIL_OK;
 }
 
 template <class Dev, class JobT>
@@ -691,40 +1003,59 @@ int upload(JobT* job, const void* host, int64_t host_row, int64_t host_rows) {
     const stencil_problem& g = job->global;
     if (host_row < g.nx + 2 * g.radius || host_rows < g.ny + 2 * g.radius)
         return set_error(STENCIL_EINVAL, "host array too small");
-    SLAB_TRY(sync_all(*job));
+    if (job->margin) {
+        const int rc = g.dtype == STENCIL_F64
+                           ? check_rolling_rings(static_cast<const double*>(host), g, host_row, host_rows)
+                           : check_rolling_rings(static_cast<const float*>(host), g, host_row, host_rows);
+        SLAB_TRY(rc);
+    }
+    SLAB_TRY(sync_bounded(*job));
+    SLAB_FAIL(*job, reset_signals(*job));
     const size_t es = g.dtype == STENCIL_F64 ? 8 : 4;
     job->cur_is_a = true;
     job->position = 0;
     for (Slab<Dev>& s : job->s) {
-        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_FAIL(*job, Dev::set_device(s.device));
         // host planes [first, first + n + 2r) hold this slab's planes -r .. n+r-1
         const char* h = static_cast<const char*>(host) + size_t(s.first) * size_t(host_row * host_rows) * es;
-        SLAB_TRY(Dev::upload(&s.l, grid_at(*job, s, 0), h, host_row, host_rows, s.sa));
+        SLAB_FAIL(*job, Dev::upload(&s.l, grid_at(*job, s, 0), h, host_row, host_rows, s.sa));
         if (job->margin)
-            SLAB_TRY(init_margin(*job, s));
+            SLAB_FAIL(*job, init_margin(*job, s));
         else
-            SLAB_TRY(Dev::upload(&s.l, s.b, h, host_row, host_rows, s.sa));
+            SLAB_FAIL(*job, Dev::upload(&s.l, s.b, h, host_row, host_rows, s.sa));
     }
-    SLAB_TRY(exchange(*job, 0));
-    if (!job->margin) SLAB_TRY(exchange(*job, 1));
-    return sync_all(*job);
+    SLAB_FAIL(*job, exchange(*job, 0));
+    if (!job->margin) SLAB_FAIL(*job, exchange(*job, 1));
+    SLAB_TRY(sync_bounded(*job));
+    clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev>
+int one_round(Job<Dev>& j, int k, bool full) {
+    SLAB_TRY(throttle(j));
+    if (j.margin)
+        SLAB_FAIL(j, j.roll_overlap ? slab_round_rolling_overlap(j, k) : slab_round_rolling(j, k));
+    else if (full && j.signal)
+        SLAB_FAIL(j, slab_round_signal(j, k));
+    else
+        SLAB_FAIL(j, slab_round(j, k));
+    SLAB_FAIL(j, mark_round(j));
+    return STENCIL_OK;
 }
 
 template <class Dev, class JobT>
 int run(JobT* job, uint32_t iterations, float* elapsed_ms) {
     if (!job) return set_error(STENCIL_EINVAL, "null job");
-    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(sync_bounded(*job));
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t done = 0;
     const uint32_t k = uint32_t(job->k);
-    for (; done + k <= iterations; done += k)
-        SLAB_TRY(job->margin ? slab_round_rolling(*job, int(k))
-                             : job->signal ? slab_round_signal(*job, int(k)) : slab_round(*job, int(k)));
+    for (; done + k <= iterations; done += k) SLAB_TRY(one_round(*job, int(k), true));
     if (done < iterations)  // the remainder as one shorter fused round
-        SLAB_TRY(job->margin ? slab_round_rolling(*job, int(iterations - done))
-                             : slab_round(*job, int(iterations - done)));
-    SLAB_TRY(sync_all(*job));
-    if (job->signal) SLAB_TRY(check_signal_timeouts(*job));
+        SLAB_TRY(one_round(*job, int(iterations - done), false));
+    SLAB_TRY(sync_bounded(*job));
+    if (job->signal) SLAB_FAIL(*job, check_signal_timeouts(*job));
     const auto t1 = std::chrono::steady_clock::now();
     if (elapsed_ms) *elapsed_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
     clear_error();
@@ -734,20 +1065,20 @@ int run(JobT* job, uint32_t iterations, float* elapsed_ms) {
 template <class Dev, class JobT>
 int download(JobT* job, void* host, int64_t host_row, int64_t host_rows) {
     if (!job || !host) return set_error(STENCIL_EINVAL, "null argument");
-    SLAB_TRY(sync_all(*job));
     const stencil_problem& g = job->global;
     const int64_t r = g.radius;
     const size_t es = g.dtype == STENCIL_F64 ? 8 : 4;
     const size_t hplane = size_t(host_row * host_rows) * es;
     if (host_row < g.nx + 2 * r || host_rows < g.ny + 2 * r) return set_error(STENCIL_EINVAL, "host array too small");
+    SLAB_TRY(sync_bounded(*job));
     std::vector<char> tmp;
     for (Slab<Dev>& s : job->s) {
-        SLAB_TRY(Dev::set_device(s.device));
+        SLAB_FAIL(*job, Dev::set_device(s.device));
         // the slab's planes -r .. n+r-1 through a scratch copy; keep its own
         // planes, plus the global ghost planes at the two ends
         tmp.resize(size_t(s.n + 2 * r) * hplane);
-        SLAB_TRY(Dev::download(&s.l, cur_grid(*job, s), tmp.data(), host_row, host_rows, s.sa));
-        SLAB_TRY(Dev::stream_sync(s.sa));
+        SLAB_FAIL(*job, Dev::download(&s.l, cur_grid(*job, s), tmp.data(), host_row, host_rows, s.sa));
+        SLAB_TRY(sync_bounded(*job));
         const int64_t z0 = s.index == 0 ? -r : 0;
         const int64_t z1 = s.index + 1 == slabs_total(*job) ? s.n + r : s.n;
         std::memcpy(static_cast<char*>(host) + size_t(s.first + z0 + r) * hplane, tmp.data() + size_t(z0 + r) * hplane,
@@ -760,7 +1091,7 @@ int download(JobT* job, void* host, int64_t host_row, int64_t host_rows) {
 template <class Dev, class JobT>
 int kernel_timing(JobT* job, int32_t enable) {
     if (!job) return set_error(STENCIL_EINVAL, "null job");
-    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(sync_bounded(*job));
     SLAB_TRY(Dev::set_device(job->s[0].device));
     drop_timing(*job);
     job->timing = enable != 0;
@@ -768,10 +1099,19 @@ int kernel_timing(JobT* job, int32_t enable) {
     return STENCIL_OK;
 }
 
+// The round form of the job's full rounds (STENCIL_SLAB_FORM_*).
+template <class Dev>
+int round_form_of(const Job<Dev>& j) {
+    return j.signal ? STENCIL_SLAB_FORM_SIGNALLED
+           : j.margin ? STENCIL_SLAB_FORM_ROLLING
+           : j.serial ? STENCIL_SLAB_FORM_SERIAL
+                      : STENCIL_SLAB_FORM_BOUNDARY_INTERIOR;
+}
+
 template <class Dev, class JobT>
 int kernel_time(JobT* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch, int32_t* signalled) {
     if (!job) return set_error(STENCIL_EINVAL, "null job");
-    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(sync_bounded(*job));
     SLAB_TRY(Dev::set_device(job->s[0].device));
     float sum = 0.f;
     for (auto& e : job->tev) {
@@ -784,24 +1124,41 @@ int kernel_time(JobT* job, float* total_ms, int64_t* launches, int64_t* cells_pe
     // per span, so `cells_per_launch` is what one span covers
     if (launches) *launches = int64_t(job->tev.size());
     if (cells_per_launch) *cells_per_launch = job->timed_cells;
-    if (signalled) *signalled = job->signal ? 1 : job->margin ? 2 : job->serial ? 3 : 0;
+    if (signalled) *signalled = job->signal ? 1 : 0;  // stencil_slab_round_form: the form
     clear_error();
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int round_form(const JobT* job, int32_t* form) {
+    if (!job || !form) return set_error(STENCIL_EINVAL, "null argument");
+    *form = round_form_of(*job);
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int set_timeout(JobT* job, int64_t ms) {
+    if (!job || ms < 1) return set_error(STENCIL_EINVAL, "null job or timeout < 1 ms");
+    job->timeout_ms = ms;
+    for (Slab<Dev>& s : job->s)
+        if (s.comm) Dev::comm_set_timeout(s.comm, ms);
     return STENCIL_OK;
 }
 
 template <class Dev, class JobT>
 int plane_sums(JobT* job, double* sums) {
     if (!job || !sums) return set_error(STENCIL_EINVAL, "null argument");
-    SLAB_TRY(sync_all(*job));
+    SLAB_TRY(sync_bounded(*job));
     for (Slab<Dev>& s : job->s) {
-        SLAB_TRY(Dev::set_device(s.device));
-        SLAB_TRY(Dev::plane_sums(&s.l, cur_grid(*job, s), sums + s.first, s.sa));
-        SLAB_TRY(Dev::stream_sync(s.sa));
+        SLAB_FAIL(*job, Dev::set_device(s.device));
+        SLAB_FAIL(*job, Dev::plane_sums(&s.l, cur_grid(*job, s), sums + s.first, s.sa));
+        SLAB_TRY(sync_bounded(*job));
     }
     clear_error();
     return STENCIL_OK;
 }
 
+#undef SLAB_FAIL
 #undef SLAB_TRY
 
 }  // namespace slab

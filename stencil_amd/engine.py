@@ -167,14 +167,18 @@ class JacobiEngine:
                    "stencil_iterate", lib=self.lib)
         return (self.b if fin.value else self.a), (ms.value if timed else None)
 
-    def prepare(self, stream=None) -> None:
-        """stencil_prepare: settle the job's one-time per-shape choices (the
+    def prepare(self, stream=None) -> dict:
+        """stencil_prepare2: settle the job's one-time per-shape choices (the
         z-chunk schedule trial) by one fused launch a -> b, then the same
         launch for ~25 ms of device time so the GPU's clock has settled
-        (DESIGN.md §6); `a` is unchanged."""
-        _lib.check(self.lib.stencil_prepare(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
-                                            ctypes.c_void_p(self.b.data_ptr()), _stream_handle(stream)),
-                   "stencil_prepare", lib=self.lib)
+        (DESIGN.md §6); `a` is unchanged.  Returns what ran: launches and
+        their estimated device ms."""
+        n, ms = ctypes.c_int64(0), ctypes.c_float(0.0)
+        _lib.check(self.lib.stencil_prepare2(ctypes.byref(self.layout), ctypes.c_void_p(self.a.data_ptr()),
+                                             ctypes.c_void_p(self.b.data_ptr()), _stream_handle(stream),
+                                             ctypes.byref(n), ctypes.byref(ms)),
+                   "stencil_prepare2", lib=self.lib)
+        return {"launches": int(n.value), "device_ms": float(ms.value)}
 
     def plan(self, iterations: int):
         launches = ctypes.c_int64(0)
@@ -453,9 +457,20 @@ class SlabJob:
         ms, n, cells, sig = ctypes.c_float(0.0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
         _lib.check(self.lib.stencil_slab_kernel_time(self.job, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(cells),
                                                      ctypes.byref(sig)), "stencil_slab_kernel_time", lib=self.lib)
-        # the round form: 0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial
+        form = self.round_form()
         return {"total_ms": float(ms.value), "launches": int(n.value), "cells_per_launch": int(cells.value),
-                "signalled": int(sig.value) == 1, "rolling": int(sig.value) == 2, "serial": int(sig.value) == 3}
+                "signalled": int(sig.value) == 1, "rolling": form == 2, "serial": form == 3, "form": form}
+
+    def round_form(self) -> int:
+        """0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial."""
+        f = ctypes.c_int32(-1)
+        _lib.check(self.lib.stencil_slab_round_form(self.job, ctypes.byref(f)), "stencil_slab_round_form", lib=self.lib)
+        return int(f.value)
+
+    def set_timeout(self, ms: int) -> None:
+        """The job's deadline for every device wait (stencil_slab_set_timeout):
+        past it the job fails with STENCIL_ETIMEOUT and aborts its communicators."""
+        _lib.check(self.lib.stencil_slab_set_timeout(self.job, int(ms)), "stencil_slab_set_timeout", lib=self.lib)
 
     def plane_sums(self) -> np.ndarray:
         out = np.zeros(self.shape[2], dtype=np.float64)

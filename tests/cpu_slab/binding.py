@@ -35,6 +35,7 @@ class FakeSlabLib:
         cdll.fake_slab_set_signal.argtypes = [ctypes.c_int32]
         cdll.fake_slab_set_free_bytes.argtypes = [ctypes.c_int64]
         cdll.fake_slab_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+        cdll.fake_slab_layout_init.argtypes = [ctypes.POINTER(_lib.Problem), ctypes.POINTER(_lib.Layout)]
 
     # what _lib.check calls on failure
     def stencil_last_error_message(self):
@@ -54,6 +55,14 @@ class FakeSlabLib:
 
     def set_free_bytes(self, b: int) -> None:
         self._cdll.fake_slab_set_free_bytes(b)
+
+    def layout(self, prob) -> "_lib.Layout":
+        """The fake device's padded layout of `prob` (its copy of api.hip's rule)."""
+        lay = _lib.Layout()
+        rc = self._cdll.fake_slab_layout_init(ctypes.byref(prob), ctypes.byref(lay))
+        if rc:
+            raise _lib.StencilError(rc, "fake_slab_layout_init", self._cdll.fake_slab_last_error_message().decode())
+        return lay
 
     def stats(self, reset: bool = False) -> dict:
         out = (ctypes.c_int64 * 5)()

@@ -96,7 +96,18 @@ Mailbox& mailbox() {
 struct Comm {
     std::string id;
     int rank = 0, nranks = 1;
+    int64_t timeout_ms = 20000;  // a receive waits this long (the job's timeout)
+    int64_t sent = 0;            // sends posted (FAKE_SLAB_MUTE_*)
 };
+
+// Test hook: FAKE_SLAB_MUTE_RANK=r, FAKE_SLAB_MUTE_AFTER=n -- rank r stops
+// posting its sends after its first n (a peer that stopped answering).
+bool muted(Comm* c) {
+    const char* r = std::getenv("FAKE_SLAB_MUTE_RANK");
+    if (!r || !*r || std::atoi(r) != c->rank) return false;
+    const char* n = std::getenv("FAKE_SLAB_MUTE_AFTER");
+    return c->sent++ >= (n && *n ? std::atoll(n) : 0);
+}
 
 struct PendingRecv {
     void* p;
@@ -145,15 +156,18 @@ int file_send(const void* p, size_t bytes, int from, int to, const std::string& 
     if (std::rename(tmp.c_str(), path.c_str()) != 0) return set_error(STENCIL_EHIP, "fake send: rename failed");
     return STENCIL_OK;
 }
-int file_take(void* p, size_t bytes, int from, int to, const std::string& id) {
+int file_take(void* p, size_t bytes, int from, int to, const std::string& id, int64_t timeout_ms) {
     int64_t seq;
     {
         std::lock_guard<std::mutex> lk(g_seq_mu);
         seq = g_taken[std::make_tuple(id, from, to)]++;
     }
     const std::string path = mail_path(id, from, to, seq);
-    for (int it = 0; access(path.c_str(), F_OK) != 0; ++it) {
-        if (it > 30000) return set_error(STENCIL_EHIP, "fake recv: rank %d waited 30 s for rank %d", to, from);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    while (access(path.c_str(), F_OK) != 0) {
+        if (std::chrono::steady_clock::now() > deadline)
+            return set_error(STENCIL_ETIMEOUT, "fake recv: rank %d waited %lld ms for rank %d", to,
+                             (long long)timeout_ms, from);
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
     std::ifstream f(path, std::ios::binary | std::ios::ate);
@@ -166,12 +180,13 @@ int file_take(void* p, size_t bytes, int from, int to, const std::string& id) {
 }
 
 int take(void* p, size_t bytes, int peer, Comm* c) {
-    if (mail_dir()) return file_take(p, bytes, peer, c->rank, c->id);
+    if (mail_dir()) return file_take(p, bytes, peer, c->rank, c->id, c->timeout_ms);
     Mailbox& m = mailbox();
     std::unique_lock<std::mutex> lk(m.mu);
     const auto key = std::make_tuple(c->id, peer, c->rank);
-    if (!m.cv.wait_for(lk, std::chrono::seconds(20), [&] { return !m.q[key].empty(); }))
-        return set_error(STENCIL_EHIP, "fake recv: rank %d waited 20 s for rank %d", c->rank, peer);
+    if (!m.cv.wait_for(lk, std::chrono::milliseconds(c->timeout_ms), [&] { return !m.q[key].empty(); }))
+        return set_error(STENCIL_ETIMEOUT, "fake recv: rank %d waited %lld ms for rank %d", c->rank,
+                         (long long)c->timeout_ms, peer);
     std::vector<char> msg = std::move(m.q[key].front());
     m.q[key].pop_front();
     if (msg.size() != bytes)
@@ -233,13 +248,34 @@ struct FakeDev {
         return *c ? STENCIL_OK : set_error(STENCIL_ENOMEM, "fake counters");
     }
     static void free_counters(uint32_t* c) { std::free(c); }
-    static int stream_create(Stream* s, bool) {
+    static int alloc_flag(uint32_t** f) {
+        *f = static_cast<uint32_t*>(std::calloc(1, sizeof(uint32_t)));
+        return *f ? STENCIL_OK : set_error(STENCIL_ENOMEM, "fake flag");
+    }
+    static void free_flag(uint32_t* f) { std::free(f); }
+    static int reset_counters(uint32_t* c, uint32_t* flag, uint64_t*) {
+        if (c) std::memset(c, 0, 4 * sizeof(uint32_t));
+        if (flag) *flag = 0;
+        return STENCIL_OK;
+    }
+    static void release_waits(uint32_t* flag, uint64_t*) {
+        if (flag) *flag = 1;
+    }
+    static int stream_create(Stream* s, int) {
         static char dummy;
         *s = &dummy;
         return STENCIL_OK;
     }
     static void stream_destroy(Stream) {}
     static int stream_sync(Stream) { return STENCIL_OK; }
+    // synchronous streams: everything has completed when it was issued (a
+    // receive that never arrives fails at issue, after the comm's timeout)
+    static int sync_until(Stream, Comm, slab::Clock::time_point) { return STENCIL_OK; }
+    static int event_sync_until(Event, Comm, slab::Clock::time_point) { return STENCIL_OK; }
+    static int default_timeout_ms() {
+        const char* v = std::getenv("STENCIL_SLAB_TIMEOUT_MS");
+        return v && std::atoi(v) > 0 ? std::atoi(v) : 20000;
+    }
     static int event_create(Event* e, bool) {
         *e = new fake::Event;
         return STENCIL_OK;
@@ -303,6 +339,10 @@ struct FakeDev {
                    ? sweep_t(l, static_cast<const double*>(src), static_cast<double*>(dst), b, e, k)
                    : sweep_t(l, static_cast<const float*>(src), static_cast<float*>(dst), b, e, k);
     }
+    static bool rolling_overlap() {
+        const char* v = std::getenv("STENCIL_SLAB_ROLLING_OVERLAP");
+        return !(v && *v && std::atoi(v) == 0);
+    }
     static bool serial_rounds() { return std::getenv("STENCIL_SLAB_SERIAL") && std::atoi(std::getenv("STENCIL_SLAB_SERIAL")); }
     static int face_signal_create(uint64_t** fs) {  // the fake waits synchronously: no signal word
         *fs = nullptr;
@@ -322,12 +362,12 @@ struct FakeDev {
         *nsig = 1;
         return STENCIL_OK;
     }
-    static int wait_counters(uint32_t* c, uint32_t lo, uint32_t hi, Stream) {
-        if (c[0] < lo || c[1] < hi) c[2] = 1;  // synchronous: a count short now never arrives
+    static int wait_counters(uint32_t* c, uint32_t* flag, uint32_t lo, uint32_t hi, Stream) {
+        if (c[0] < lo || c[1] < hi) *flag = 1;  // synchronous: a count short now never arrives
         return STENCIL_OK;
     }
-    static int read_timeout(uint32_t* c, bool* timed_out) {
-        *timed_out = c[2] != 0;
+    static int read_timeout(uint32_t* flag, bool* timed_out) {
+        *timed_out = *flag != 0;
         return STENCIL_OK;
     }
     static int copy_d2d(void* dst, const void* src, size_t bytes, Stream) {
@@ -446,6 +486,8 @@ struct FakeDev {
         return STENCIL_OK;
     }
     static void comm_destroy(Comm c) { delete c; }
+    static void comm_abort(Comm c) { delete c; }  // as ncclCommAbort: the comm is gone
+    static void comm_set_timeout(Comm c, int64_t ms) { c->timeout_ms = ms; }
     static int group_start() {
         ++fake::t_group;
         return STENCIL_OK;
@@ -461,6 +503,7 @@ struct FakeDev {
     }
     static int send(const void* p, size_t bytes, int peer, Comm c, Stream) {
         if (peer < 0 || peer >= c->nranks) return set_error(STENCIL_EINVAL, "fake send to rank %d of %d", peer, c->nranks);
+        if (fake::muted(c)) return STENCIL_OK;  // the test's silent peer
         if (fake::mail_dir()) {
             std::lock_guard<std::mutex> lk(fake::g_stat_mu);
             ++fake::g_sends;
@@ -566,5 +609,9 @@ int fake_slab_kernel_time(fake_slab_job* job, float* ms, int64_t* n, int64_t* ce
     return core::kernel_time<FakeDev>(job, ms, n, cells, sig);
 }
 int fake_slab_plane_sums(fake_slab_job* job, double* sums) { return core::plane_sums<FakeDev>(job, sums); }
+// the fake's layout arithmetic, compared with the product's stencil_layout_init
+int fake_slab_layout_init(const stencil_problem* p, stencil_layout* out) { return FakeDev::layout_init(p, out); }
+int fake_slab_round_form(const fake_slab_job* job, int32_t* form) { return core::round_form<FakeDev>(job, form); }
+int fake_slab_set_timeout(fake_slab_job* job, int64_t ms) { return core::set_timeout<FakeDev>(job, ms); }
 
 }  // extern "C"

@@ -452,3 +452,35 @@ def test_rolling_slabs_equal_one_grid(gpu, dtype, shape, nslabs):
         finally:
             job.close()
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), margin
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+def test_cpwait_one_chunk_slab_counts_both_faces(gpu, monkeypatch, shape):
+    """in a slab of exactly K planes on one tile, one
+    workgroup stores both faces at the same plane step; its face-signal add
+    must count 2 (it added 1, and the command-processor wait of
+    STENCIL_SLAB_CPWAIT=1 then never returned).  A 20 s job deadline turns a
+    regression into a failure instead of a hang."""
+    monkeypatch.setenv("STENCIL_SLAB_TIMEOUT_MS", "20000")
+    nx, ny = 40, 24  # one x-y tile
+    k = JacobiEngine(StencilSpec(dims=3, dtype="fp64", shape=shape), nx, ny, 8, device=gpu, allocate=False).fuse_steps
+    it = 3 * k + 1
+    want = _periodic_job(gpu, monkeypatch, nx, ny, k, it, False, shape=shape)
+    monkeypatch.setenv("STENCIL_SLAB_CPWAIT", "1")
+    got = _periodic_job(gpu, monkeypatch, nx, ny, k, it, True, shape=shape)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+@pytest.mark.parametrize("xcu,excl", [(1, "0"), (2, "1")])
+@pytest.mark.parametrize("exchange", ["copy", "rccl"])
+@pytest.mark.parametrize("signalled", [True, False])
+def test_exchange_on_a_cu_masked_stream(gpu, monkeypatch, xcu, excl, exchange, signalled):
+    """STENCIL_SLAB_XCU: the exchange (and the face wait) on a stream confined
+    to `xcu` CUs of every XCD, the launches' streams off them with
+    STENCIL_SLAB_XCU_EXCL=1 -- bitwise the unmasked rounds."""
+    nx, ny, nz, it = 130, 64, 20, 9
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False)
+    monkeypatch.setenv("STENCIL_SLAB_XCU", str(xcu))
+    monkeypatch.setenv("STENCIL_SLAB_XCU_EXCL", excl)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, signalled, exchange=exchange)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))

@@ -135,11 +135,14 @@ def test_periodic_ring_equals_replicated_grid(fake, nslabs, exchange):
 @pytest.mark.parametrize("dtype,shape,k", [("fp64", "star", 4), ("fp32", "box", 3)])
 @pytest.mark.parametrize("nslabs", [1, 2, 3])
 @pytest.mark.parametrize("margin_extra", [1, 3, 40])
-def test_rolling_slabs_equal_one_grid(fake, dtype, shape, k, nslabs, margin_extra):
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_rolling_slabs_equal_one_grid(fake, monkeypatch, dtype, shape, k, nslabs, margin_extra, overlap):
     """ROLLING: one resident grid per slab plus a margin -- from one-plane
     launches (margin = K r + 1) to one launch per pass; down and up passes,
-    remainder passes, the halo exchange after each pass and the global ends'
-    ghost restores; bitwise the oracle's one grid."""
+    remainder passes, the halo exchange (overlapped: faces computed into a
+    staging buffer first and exchanged beside the pass; or after the pass)
+    and the global ends' ghost restores; bitwise the oracle's one grid."""
+    monkeypatch.setenv("STENCIL_SLAB_ROLLING_OVERLAP", overlap)
     fake.set_k(k)
     spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
     nx, ny, nz = 11, 5, 7 * nslabs + 1
@@ -154,7 +157,14 @@ def test_rolling_slabs_equal_one_grid(fake, dtype, shape, k, nslabs, margin_extr
         fake.stats(reset=True)
         job.run(it)
         sweeps += it
-        assert fake.stats()["signal_sweeps"] == 0  # rolling rounds are plain passes
+        st = fake.stats()
+        assert st["signal_sweeps"] == 0  # rolling rounds are plain passes
+        # launches per pass: the z-range launches, plus one face launch per
+        # shared face when overlapped
+        rounds = -(-it // k)
+        faces = 2 * (nslabs - 1) if overlap == "1" else 0
+        per_pass = sum(-(-(nz // nslabs + (1 if r < nz % nslabs else 0)) // margin_extra) for r in range(nslabs))
+        assert st["sweeps"] == rounds * (per_pass + faces), st
         assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps, seed=3))
     job.kernel_timing(True)
     job.run(k)
@@ -200,13 +210,16 @@ def _rank_jobs(fake, spec, grid, nranks, fn, rolling=False, margin=0):
 
 
 @pytest.mark.parametrize("nranks", [2, 3])
-@pytest.mark.parametrize("rolling", [False, True])
+@pytest.mark.parametrize("rolling", [False, True, "serial"])
 @pytest.mark.parametrize("shape", ["star", "box"])
-def test_rank_mode_equals_one_grid(fake, nranks, rolling, shape):
+def test_rank_mode_equals_one_grid(fake, monkeypatch, nranks, rolling, shape):
     """Rank mode (stencil_slab_create_rank: one slab per process, peers by
     global index, as torch.distributed.run launches bench.py on the 8-GPU
     node), one thread per rank: each rank's planes, assembled, bitwise the
     oracle's one grid; face-signalled rounds when not rolling."""
+    if rolling == "serial":  # rolling rounds with the exchange after the pass
+        monkeypatch.setenv("STENCIL_SLAB_ROLLING_OVERLAP", "0")
+        rolling = True
     k = 4 if shape == "star" else 3
     fake.set_k(k)
     spec = StencilSpec(dims=3, dtype="fp64", shape=shape)
@@ -262,3 +275,114 @@ def test_exchange_counts_per_round(fake):
         faces = 2 * n if periodic else 2 * (n - 1)
         assert st["sends"] == st["recvs"] == 2 * faces, (periodic, n, st)
         job.close()
+
+
+# ---- round 5: bounded-time failure, the rolling upload check, round forms, layout
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("rolling", [False, True])
+def test_silent_peer_fails_every_rank_in_bounded_time(fake, monkeypatch, nranks, rolling):
+    """A rank that stops posting its sends (FAKE_SLAB_MUTE_RANK) after the
+    fill's exchange: every rank's run() returns STENCIL_ETIMEOUT within the
+    job's deadline -- the ranks waiting on it directly, the muted rank once the
+    others stopped (fail fast; stencil_rma.cpp:334-338's
+    never-waited reply hangs instead).  Later calls fail at once; destroy works."""
+    import time
+    k = 4
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    muted = nranks - 1  # the top rank: one neighbour, one send per exchange
+    monkeypatch.setenv("FAKE_SLAB_MUTE_RANK", str(muted))
+    monkeypatch.setenv("FAKE_SLAB_MUTE_AFTER", "1" if rolling else "2")  # the fill's exchanges
+    timeout_ms = 800
+
+    def fn(job, r):
+        job.set_timeout(timeout_ms)
+        job.fill_initial("reference")
+        t0 = time.monotonic()
+        try:
+            job.run(6 * k)
+            return ("ok", time.monotonic() - t0, None)
+        except _lib.StencilError as exc:
+            took = time.monotonic() - t0
+            try:
+                job.run(k)
+                again = "ran"
+            except _lib.StencilError as exc2:
+                again = exc2.code, str(exc2)
+            return (exc.code, took, again)
+
+    out, errs = _rank_jobs(fake, spec, (8, 6, 8 * nranks), nranks, fn, rolling=rolling, margin=k + 2)
+    assert not any(errs), errs
+    for r, (code, took, again) in enumerate(out):
+        assert code == _lib.ETIMEOUT, (r, out)
+        # a rank waits at most one deadline per receive it is blocked on, and
+        # the muted rank only notices once a neighbour has given up
+        assert took < 3 * timeout_ms / 1000 + 1.0, (r, took)
+        assert again[0] == _lib.ETIMEOUT and "failed earlier" in again[1], again
+
+
+def test_upload_checks_the_rolling_ghost_ring(fake):
+    """ROLLING slabs need the same x/y ghost ring in every plane:
+    upload refuses a host grid whose ring varies with z, and takes it for a
+    two-grid job, where it is computed right."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 9, 6, 12
+    p1 = ob.problem(3, "fp64", "star", 1, "naive", nx, ny, nz)
+    good = ob.init(p1, "random", 5)
+    bad = good.copy()
+    bad[7, 0, 3] = 0.5  # a y-ghost cell of plane 6
+    job = SlabJob(spec, nx, ny, nz, [0, 1], exchange="rccl", rolling=True, margin=8, lib=fake)
+    job.upload(good)
+    with pytest.raises(_lib.StencilError, match="same x/y ghost ring"):
+        job.upload(bad)
+    job.close()
+    two = SlabJob(spec, nx, ny, nz, [0, 1], exchange="rccl", lib=fake)
+    two.upload(bad)
+    two.run(5)
+    want = bad.copy()
+    a, b = want, want.copy()
+    for _ in range(5):
+        ob.sweep(p1, a, b, 0, nz)
+        a, b = b, a
+    assert_bitwise(two.download(), a)
+    two.close()
+
+
+@pytest.mark.parametrize("case,form", [
+    (dict(devs=[0, 1]), 1),                      # distinct devices: face-signalled
+    (dict(devs=[0, 0], exchange="copy"), 0),     # shared: boundary + interior
+    (dict(devs=[0, 1], rolling=True), 2),
+    (dict(devs=[0, 1], serial=True), 3),
+])
+def test_round_form_and_signalled_flag(fake, monkeypatch, case, form):
+    """stencil_slab_round_form gives the form; kernel_time's `signalled`
+    stays 0/1 (it had become the form code)."""
+    fake.set_k(4)
+    if case.get("serial"):
+        monkeypatch.setenv("STENCIL_SLAB_SERIAL", "1")
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 8, 6, 16, case["devs"], exchange=case.get("exchange", "rccl"),
+                  rolling=case.get("rolling", False), margin=6 if case.get("rolling") else 0, lib=fake)
+    job.fill_initial("reference")
+    job.kernel_timing(True)
+    job.run(4)
+    kt = job.kernel_time()
+    assert job.round_form() == form == kt["form"]
+    assert kt["signalled"] == (form == 1)
+    job.close()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+def test_fake_layout_is_the_product_layout(fake, dtype):
+    """The fake device's layout arithmetic is api.hip's, the row-pitch rule
+    included, over widths around every padded pitch class."""
+    widths = [1, 7, 64, 500, 512, 2048, 3000, 4000, 4080, 4096, 4100, 8176, 8192, 8200, 16384]
+    for nx in widths:
+        for r, halo in ((1, 0), (1, 4), (2, 0)):
+            prob = _lib.make_problem(dims=3, dtype=_lib.F64 if dtype == "fp64" else _lib.F32, radius=r,
+                                     nx=nx, ny=5, nz=9, halo=halo)
+            want, got = _lib.make_layout(prob), fake.layout(prob)
+            for f, _ in _lib.Layout._fields_[1:]:
+                assert getattr(got, f) == getattr(want, f), (nx, r, halo, f)

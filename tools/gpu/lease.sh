@@ -27,6 +27,8 @@
 #   loop:<cfg>       bench.py --config <cfg> --exchange loopback (the whole grid as one periodic slab: an interior rank)
 #   slabgap          tools/slab_gap.py: one K = 4 launch plain / slab layout / halo flags / signalled / slab job
 #   c1ab             tools/c1_ab.py: the C1 region variants (branch-free ghost selects) interleaved, fp64 + fp32
+#   xr:<cfg>:<N>:<ex>:<var>[:trace]  bench.py --rank-of N (0: none) --exchange loopback|nccl-self with the round
+#                    variant ovl | serial | xcu<C>[x] (STENCIL_SLAB_XCU[_EXCL]), optionally under a kernel trace
 #   c1probe          tools/c1_probe.py (C1 wall vs device time, eager vs one graph), then under a kernel trace
 set -o pipefail
 TAG=$1; shift
@@ -129,6 +131,40 @@ for step in "$@"; do
     c1probe) timeout -k 10 120 python3 tools/c1_probe.py > "$O/c1_probe.txt" 2>&1 &&
              (cd /tmp && TMPDIR=/tmp timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d "$O/c1trace" \
                -o run -- python3 "$R/tools/c1_probe.py" --reps 10 > "$O/c1_probe_traced.txt" 2>&1) ;;
+    xr:*) # xr:<cfg>:<N>:<exchange>:<variant>[:trace] -- round-5 rehearsal matrix: one interior rank of the
+          # N-GPU job (N = 0: the config's whole grid as one periodic slab) with loopback / nccl-self halos;
+          # variant ovl (default rounds) | serial | xcu<C> | xcu<C>x (exchange on C CUs per XCD, x: launches off them)
+          IFS=':' read -r c nr ex var tr <<< "${step#xr:}"
+          envs=()
+          case "$var" in
+            ovl) ;; serial) envs=(STENCIL_SLAB_SERIAL=1) ;;
+            xcu*x) cc=${var#xcu}; envs=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
+            xcu*) envs=(STENCIL_SLAB_XCU=${var#xcu}) ;;
+            *) echo "bad variant $var"; exit 2 ;;
+          esac
+          case "$c" in C5) a="--steps 16 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+          [ "$nr" != 0 ] && a="$a --rank-of $nr"
+          name="xr_${c}_${nr}_${ex}_${var}${tr:+_$tr}"
+          if [ "$tr" = trace ]; then
+            (cd /tmp && env "${envs[@]}" TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv \
+               -d "$O/$name" -o run -- python3 "$R/bench.py" --config "$c" --exchange "$ex" $a --no-cpu-baseline \
+               > "$O/$name.json" 2>> "$O/bench.err")
+          else
+            env "${envs[@]}" timeout -k 10 400 python3 bench.py --config "$c" --exchange "$ex" $a --no-cpu-baseline \
+              > "$O/$name.json" 2>> "$O/bench.err"
+          fi ;;
+    xcdab:*) # xcdab:<dtype>:nx:ny:nz:steps -- the strip kernel's XCD-patch tile order (STENCIL_TK_XCD=w), interleaved
+          IFS=':' read -r dt nx ny nz st <<< "${step#xcdab:}"
+          timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 5 --launches 3 \
+            --variant STENCIL_TK_XCD=0 --variant STENCIL_TK_XCD=2 --variant STENCIL_TK_XCD=4 --variant STENCIL_TK_XCD=8 \
+            --variant STENCIL_TK_XCD=16 > "$O/xcd_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
+    xcdpmc:*) # xcdpmc:<dtype>:nx:ny:nz:steps:w -- FETCH_SIZE / WRITE_SIZE passes of that variant's launches
+          IFS=':' read -r dt nx ny nz st w <<< "${step#xcdpmc:}"
+          for ctr in FETCH_SIZE WRITE_SIZE; do
+            (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --pmc $ctr --output-format csv \
+               -d "$O/xcdpmc_${dt}_w${w}_$ctr" -o run -- python3 "$R/tools/ab.py" --dtype "$dt" --grid "$nx" "$ny" "$nz" \
+               --steps "$st" --reps 1 --launches 3 --variant STENCIL_TK_XCD=$w > "$O/xcdpmc_${dt}_w${w}_$ctr.log" 2>&1) || exit 1
+          done ;;
     tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
              --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
