@@ -889,9 +889,24 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
     else:
         out["cpu_baseline"] = None
     if emit:
-        print(json.dumps(out), flush=True)
+        _JSON_OUT.write(json.dumps(out) + "\n")
+        _JSON_OUT.flush()
     return out
 
 
+# The one JSON line goes to the process's original stdout; everything else
+# written to fd 1 while the bench runs -- RCCL prints a version banner there
+# when a communicator is created -- is sent to stderr (see __main__ below).
+_JSON_OUT = sys.stdout
+
+
+def _route_stdout_to_stderr():
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 if __name__ == "__main__":
+    _route_stdout_to_stderr()
     main()

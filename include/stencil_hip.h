@@ -66,9 +66,11 @@ int stencil_last_error(void);
  * STENCIL_SLAB_CPWAIT=1 (face-signalled slab rounds wait for the faces in the
  * command processor, hipStreamWaitValue64, instead of a polling wait kernel),
  * STENCIL_SLAB_SERIAL=1 (every full slab round as one plain launch, then the
- * exchange: nothing runs beside the launch), STENCIL_SLAB_XCU=c (the slab
- * exchange's stream confined to c CUs of every XCD, 0 = not confined) and
- * STENCIL_SLAB_XCU_EXCL=1 (the launches' streams kept off those CUs),
+ * exchange: nothing runs beside the launch), STENCIL_SLAB_XCU=c (default 1:
+ * a face-signalled job whose launch takes several rounds of workgroups runs
+ * its exchange confined to c CUs of every XCD and its launches off them;
+ * 0 = never confined) and STENCIL_SLAB_XCU_EXCL=0 (the launches may use the
+ * exchange's CUs too),
  * STENCIL_SLAB_TIMEOUT_MS (a slab job's deadline for any device wait,
  * default 60000: stencil_slab_set_timeout), STENCIL_SLAB_ROLLING_OVERLAP=0
  * (rolling slab rounds exchange after the pass instead of beside it). */

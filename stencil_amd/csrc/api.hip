@@ -306,6 +306,26 @@ __global__ void __launch_bounds__(256) copy_kernel(f32x4* __restrict__ dst, cons
 
 using namespace stencil;
 
+namespace stencil {
+int signal_launch_geometry(const stencil_layout& l, int64_t begin, int64_t end, int steps, int64_t* tiles,
+                           int64_t* workgroups, int* slots) {
+    LaunchInfo info;
+    tl_dry_launch = &info;
+    int nsig = 0;
+    void* fake_out = reinterpret_cast<void*>(uintptr_t(1));  // never touched in a dry launch
+    const int rc = box27_supports(l.prob)
+                       ? launch_boxk_signal(l, nullptr, fake_out, begin, end, steps, nullptr, nullptr, &nsig, nullptr)
+                       : launch_tkstrip_signal(l, nullptr, fake_out, begin, end, steps, nullptr, nullptr, &nsig, nullptr);
+    tl_dry_launch = nullptr;
+    if (rc != STENCIL_OK) return rc;
+    if (info.steps == 0) return set_error(STENCIL_EUNSUPPORTED, "no face-signalled launch was described");
+    *tiles = nsig;  // one face signal per tile and face
+    *workgroups = info.workgroups;
+    *slots = info.slots;
+    return STENCIL_OK;
+}
+}  // namespace stencil
+
 extern "C" {
 
 const char* stencil_strerror(int code) {
@@ -552,6 +572,7 @@ int stencil_sweepk_geometry(const stencil_layout* l, int64_t begin, int64_t end,
     clear_error();
     return STENCIL_OK;
 }
+
 
 int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
                           int32_t steps, uint32_t* counters, uint64_t* face_signal, int32_t* signals_per_face,

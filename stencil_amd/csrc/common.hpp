@@ -75,8 +75,16 @@ struct LaunchInfo {
     int zchunk = 0;   // planes per z-chunk; 0 = one balanced share per workgroup
     int packed = 0;   // 0 equal chunks, 1 packed (measured faster), 2 packed by the model, not yet measured
     int steps = 0;
+    int slots = 0;    // resident workgroups of the kernel on the device (one round)
 };
 extern thread_local LaunchInfo* tl_dry_launch;
+
+// A face-signalled slab launch's geometry (a dry launch: nothing runs):
+// x-y tiles, workgroups and one round's resident slots.  slab.hip confines a
+// job's exchange to a few CUs when the launch beside it takes several rounds
+// of workgroups (slab_core.hpp).
+int signal_launch_geometry(const stencil_layout& l, int64_t begin, int64_t end, int steps, int64_t* tiles,
+                           int64_t* workgroups, int* slots);
 
 // The packed longest-first z-chunk schedule (kernels_strip.hip): for a grid of
 // few tiles, chunks of Lc planes per tile (the last one shorter) dispatched

@@ -114,13 +114,15 @@ __global__ void __launch_bounds__(64 * NW)
     const int t = blockIdx.x;
     const int bx = t % tiles_x;
     const int by = (t / tiles_x) % tiles_y;
-    const int bz = t / (tiles_x * tiles_y);
+    const int nch = (zend - zbeg + zchunk - 1) / zchunk;
+    int bz = t / (tiles_x * tiles_y);
+    // face-signalled launches: the two face chunks dispatched first (kernels_strip.hip)
+    if (SIG && nch >= 3) bz = bz == 0 ? 0 : bz == 1 ? nch - 1 : bz - 1;
     const int lane = threadIdx.x, w = threadIdx.y;
     const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
     const int64_t y0 = int64_t(by) * TY - K;
     const int za = zbeg + bz * zchunk;
     const int zb = za + zchunk < zend ? za + zchunk : zend;
-    const int nch = (zend - zbeg + zchunk - 1) / zchunk;
     const bool rev = SIG && nch >= 2 && bz == nch - 1;  // this workgroup's chunk marches down
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
@@ -398,8 +400,9 @@ __global__ void __launch_bounds__(64 * NW)
             za = zbeg + int(c) * zchunk;
         } else {
             const int bz = t / (tiles_x * tiles_y);
-            za = zbeg + bz * zchunk;
             t -= bz * tiles_x * tiles_y;
+            // face-signalled launches: the two face chunks dispatched first (kernels_strip.hip)
+            za = zbeg + (SIG && nch >= 3 ? (bz == 0 ? 0 : bz == 1 ? nch - 1 : bz - 1) : bz) * zchunk;
         }
         zb = za + zchunk < zend ? za + zchunk : zend;
     }
@@ -676,11 +679,17 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (SIG) {
             // face-signalled slab rounds: the most chunks that fit ONE round
             // with a CU per XCD to spare (the exchange runs beside the launch,
-            // kernels_strip.hip)
+            // kernels_strip.hip); a grid of several rounds: at least 4 chunks,
+            // whose two face chunks go first (the kernel's chunk order)
             const int64_t room = slots - slots / 32;
             for (int64_t c = 1; tiles * c <= room && c <= nz; ++c) {
                 if (c > 1 && (nz + c - 1) / c < 3 * K) break;
                 best_c = c;
+            }
+            if (tiles > room) {
+                int64_t want = env_int("STENCIL_BOXK_SIG_CHUNKS", 4);
+                while (want > 1 && (nz + want - 1) / want < 3 * K) --want;
+                best_c = std::max(best_c, want);
             }
         }
         zc = int((nz + best_c - 1) / best_c);
@@ -715,6 +724,16 @@ int launch_bk(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 8) return set_error(STENCIL_EINVAL, "grid too large for the box kernel");
+    if (LaunchInfo* info = tl_dry_launch) {  // describe, do not launch
+        if (slots == 0)
+            if (const int rc = resident_slots(kern, 64 * NW, &slots)) return rc;
+        info->workgroups = nb;
+        info->zchunk = zc;
+        info->packed = sched != nullptr;
+        info->steps = K;
+        info->slots = slots;
+        return STENCIL_OK;
+    }
     // XCD-patch work order for equal-chunk strip launches: 2048^2 x 256 fp64
     // K = 4 cuts L2-miss reads from 18.6 to 10.6 GB per launch (2.16x -> 1.23x
     // compulsory) and the launch time by 3 % (6.12 -> 5.93 ms; widths 2 / 8:

@@ -241,9 +241,15 @@ __global__ void __launch_bounds__(64 * NW)
             const int64_t sw = tiles_x - strip * xcd_pw < xcd_pw ? tiles_x - strip * xcd_pw : xcd_pw;
             t = rem / sw * tiles_x + strip * xcd_pw + rem % sw;
         }
+        const int64_t nch = (nzr + zchunk - 1) / zchunk;
+        // face-signalled launches of several chunks per tile: the two face
+        // chunks (the first, marching up, and the last, marching down) are
+        // dispatched as the first two generations, the middle chunks after
+        // them, so the faces are stored early even when the grid takes many
+        // rounds of workgroups
+        if (SIG && nch >= 3) c = c == 0 ? 0 : c == 1 ? nch - 1 : c - 1;
         lo = t * nzr + c * zchunk;
         hi = lo + (zchunk < nzr - c * zchunk ? zchunk : nzr - c * zchunk);
-        const int64_t nch = (nzr + zchunk - 1) / zchunk;
         rev = SIG && nch >= 2 && c == nch - 1;
     } else {
         const int64_t units = tiles * nzr;
@@ -674,6 +680,16 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
                     if (c > 1 && (nz + c - 1) / c < 2 * K) break;
                     best_c = c;
                 }
+                // a face-signalled grid of several rounds (4096^2 planes: ~6400
+                // tiles): at least 4 chunks per tile, whose two face chunks the
+                // kernel dispatches first, so the faces are stored about halfway
+                // through the launch instead of in its last round (+2 % plane
+                // steps for the extra chunk fills)
+                if (SIG && tiles > room) {
+                    int64_t want = senv_int("STENCIL_TK_SIG_CHUNKS", 4);
+                    while (want > 1 && (nz + want - 1) / want < 2 * K) --want;
+                    best_c = std::max(best_c, want);
+                }
             }
             zc = int((nz + best_c - 1) / best_c);
             nb = tiles * ((nz + zc - 1) / zc);
@@ -732,6 +748,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         info->zchunk = zc;
         info->packed = sched == nullptr ? 0 : (verdict && verdict->load() == kPackUntested ? 2 : 1);
         info->steps = K;
+        info->slots = slots;
         return STENCIL_OK;
     }
     const int xcd_pw = !SIG && zc > 0 ? senv_int("STENCIL_TK_XCD", 0) : 0;

@@ -121,6 +121,34 @@ struct HipDev {
         return 1;
     }
     static bool signal_enabled() { return api_knob("STENCIL_SLAB_SIGNAL", 1) != 0; }
+    // Confine the exchange of this job (STENCIL_SLAB_XCU CUs per XCD, default
+    // 1, for the exchange; the launches off them) when its face-signalled
+    // launch takes several rounds of workgroups: more tiles than one round
+    // holds with a CU per XCD to spare.  A one-round grid keeps every CU
+    // (512^3: 1102 Gcell/s unconfined, 1022 confined; its grid is sized for
+    // a spare CU per XCD already).  STENCIL_SLAB_XCU=0: never.
+    static bool confine_exchange(const stencil_layout& l, int k) {
+        if (xcu() == 0) return false;
+        int64_t tiles = 0, wg = 0;
+        int slots = 0;
+        if (signal_launch_geometry(l, 0, l.prob.nz, k, &tiles, &wg, &slots) != STENCIL_OK) {
+            clear_error();
+            return false;
+        }
+        return slots > 0 && tiles > slots - slots / 32;
+    }
+    // STENCIL_SLAB_WIRE_GBPS=r (debug library, rehearsals): before each
+    // exchange, a one-lane spin for one face's bytes at r GB/s on the
+    // exchange stream -- the transfer time of a face between distinct GPUs
+    // over xGMI, which a rehearsal's transfer to itself does not have
+    static int wire_delay(Stream s, size_t face_bytes) {
+        const int r = knob("STENCIL_SLAB_WIRE_GBPS", 0);
+        if (r <= 0) return STENCIL_OK;
+        const uint64_t us = uint64_t(double(face_bytes) / (double(r) * 1e3));
+        hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, us * 100);
+        STENCIL_HIP_CHECK(hipGetLastError());
+        return STENCIL_OK;
+    }
     // STENCIL_SLAB_SERIAL=1: every full round as one plain launch of the whole
     // slab followed by the exchange (no overlap)
     static bool serial_rounds() { return api_knob("STENCIL_SLAB_SERIAL", 0) != 0; }
@@ -199,10 +227,12 @@ struct HipDev {
     // RCCL's and the copies' kernels run there and not on the CUs a
     // one-per-CU launch beside them counts on; STENCIL_SLAB_XCU_EXCL=1 also
     // keeps the launches' streams off those CUs.
-    static int xcu() { return std::max(0, std::min(16, api_knob("STENCIL_SLAB_XCU", 0))); }
-    static int stream_create(Stream* s, int role) {
-        const int c = xcu();
-        const bool excl = c > 0 && api_knob("STENCIL_SLAB_XCU_EXCL", 0) != 0;
+    static int xcu() { return std::max(0, std::min(16, api_knob("STENCIL_SLAB_XCU", 1))); }
+    static int stream_create(Stream* s, int role, bool confine) {
+        // STENCIL_SLAB_XCU_EXCL=0 (with a confined exchange): the launches may
+        // use the exchange's CUs too
+        const int c = confine ? xcu() : 0;
+        const bool excl = c > 0 && api_knob("STENCIL_SLAB_XCU_EXCL", 1) != 0;
         if (role == slab::STREAM_EXCHANGE ? c > 0 : excl) {
             int dev = 0, cus = 0;
             STENCIL_HIP_CHECK(hipGetDevice(&dev));

@@ -107,6 +107,7 @@ struct Job {
     int64_t margin = 0;
     int position = 0;
     bool roll_overlap = false;  // rolling rounds with the exchange beside the pass (staged faces)
+    bool confine = false;       // the exchange on a few CUs of its own, the launches off them
     std::vector<Slab<Dev>> s;
     // kernel timing: events around slab 0's compute launch(es) of every round
     bool timing = false;
@@ -225,6 +226,8 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
         SLAB_TRY(Dev::event_record(s.ev_xin, s.sa));
         SLAB_TRY(Dev::stream_wait(s.sx, s.ev_xin));
         SLAB_TRY(pre(s));
+        // tests / rehearsals: the transfer's wire time between distinct GPUs (a no-op unless asked for)
+        SLAB_TRY(Dev::wire_delay(s.sx, size_t(d) * plane_bytes(s)));
         SLAB_TRY(Dev::event_record(s.ev_join, s.sx));  // this slab's faces are ready
     }
     if (j.exchange == STENCIL_EXCHANGE_RCCL) {
@@ -477,6 +480,7 @@ int slab_round_rolling_overlap(Job<Dev>& j, int k) {
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
         SLAB_TRY(Dev::stream_wait(s.sx, s.ev_join));
+        SLAB_TRY(Dev::wire_delay(s.sx, size_t(d) * plane_bytes(s)));  // rehearsals: a distinct GPU's wire time
     }
     if (j.exchange == STENCIL_EXCHANGE_RCCL) {
         SLAB_TRY(Dev::group_start());
@@ -733,6 +737,21 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         j->serial = !rolling && Dev::serial_rounds();
         j->signal = g.radius == 1 && g.order == STENCIL_ORDER_NAIVE && (star || box) && distinct && !rolling &&
                     !j->serial && Dev::signal_enabled();
+        // A face-signalled launch that takes several rounds of workgroups
+        // (4096^2 planes: ~6400 tiles) runs with the exchange -- its face
+        // wait and RCCL's kernels -- confined to a few CUs the launch does not
+        // use: a helper wave resident on a CU the launch's dispatch is
+        // waiting for holds up the whole launch (NS4096 rank of 4: 61 ms per
+        // launch unconfined, 54 confined, 50 alone).  Decided
+        // from the global problem's largest slab, the same on every rank.
+        if (j->signal && g.nz / total >= j->depth) {
+            stencil_problem p = g;
+            p.nz = g.nz / total + (g.nz % total ? 1 : 0);
+            p.halo = j->depth;
+            p.flags = STENCIL_HALO_LO | STENCIL_HALO_HI;
+            stencil_layout l{};
+            if (Dev::layout_init(&p, &l) == STENCIL_OK) j->confine = Dev::confine_exchange(l, j->k);
+        }
     }
     j->timeout_ms = Dev::default_timeout_ms();
     const int64_t base = g.nz / total, rem = g.nz % total;
@@ -778,8 +797,9 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         } else {
             if ((rc = Dev::alloc(s.l.bytes + 256, &s.a)) || (rc = Dev::alloc(s.l.bytes + 256, &s.b))) break;
         }
-        if ((rc = Dev::stream_create(&s.sa, STREAM_BOUNDARY)) || (rc = Dev::stream_create(&s.sb, STREAM_INTERIOR)) ||
-            (rc = Dev::stream_create(&s.sx, STREAM_EXCHANGE)) || (rc = Dev::event_create(&s.ev_bnd, false)) ||
+        if ((rc = Dev::stream_create(&s.sa, STREAM_BOUNDARY, j->confine)) ||
+            (rc = Dev::stream_create(&s.sb, STREAM_INTERIOR, j->confine)) ||
+            (rc = Dev::stream_create(&s.sx, STREAM_EXCHANGE, j->confine)) || (rc = Dev::event_create(&s.ev_bnd, false)) ||
             (rc = Dev::event_create(&s.ev_int, false)) || (rc = Dev::event_create(&s.ev_join, false)) ||
             (rc = Dev::event_create(&s.ev_xin, false)) || (rc = Dev::event_create(&s.ev_xout, false)))
             break;

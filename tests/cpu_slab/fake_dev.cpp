@@ -234,6 +234,8 @@ struct FakeDev {
         return p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4;
     }
     static bool signal_enabled() { return fake::g_signal; }
+    static bool confine_exchange(const stencil_layout&, int) { return false; }  // the fake has no CUs
+    static int wire_delay(Stream, size_t) { return STENCIL_OK; }
     static int free_bytes(int64_t* out) {
         *out = fake::g_free;
         return STENCIL_OK;
@@ -261,7 +263,7 @@ struct FakeDev {
     static void release_waits(uint32_t* flag, uint64_t*) {
         if (flag) *flag = 1;
     }
-    static int stream_create(Stream* s, int) {
+    static int stream_create(Stream* s, int, bool) {
         static char dummy;
         *s = &dummy;
         return STENCIL_OK;

@@ -471,16 +471,19 @@ def test_cpwait_one_chunk_slab_counts_both_faces(gpu, monkeypatch, shape):
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
 
 
-@pytest.mark.parametrize("xcu,excl", [(1, "0"), (2, "1")])
-@pytest.mark.parametrize("exchange", ["copy", "rccl"])
-@pytest.mark.parametrize("signalled", [True, False])
-def test_exchange_on_a_cu_masked_stream(gpu, monkeypatch, xcu, excl, exchange, signalled):
-    """STENCIL_SLAB_XCU: the exchange (and the face wait) on a stream confined
-    to `xcu` CUs of every XCD, the launches' streams off them with
-    STENCIL_SLAB_XCU_EXCL=1 -- bitwise the unmasked rounds."""
-    nx, ny, nz, it = 130, 64, 20, 9
-    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False)
-    monkeypatch.setenv("STENCIL_SLAB_XCU", str(xcu))
-    monkeypatch.setenv("STENCIL_SLAB_XCU_EXCL", excl)
-    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, signalled, exchange=exchange)
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("xcu", ["1", "0"])
+def test_many_round_signalled_launch_face_chunks_first(gpu, monkeypatch, shape, dtype, xcu):
+    """A face-signalled launch of a plane with more tiles than one round of
+    workgroups (2048 x 1024: ~800 tiles) splits every tile into at least 4
+    z-chunks and dispatches the two face chunks first (slab rounds then
+    confine the exchange to one CU per XCD, STENCIL_SLAB_XCU): bitwise the
+    boundary + interior rounds."""
+    monkeypatch.setenv("STENCIL_SLAB_XCU", xcu)
+    nx, ny, nz, it = 2048, 1024, 40, 9
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape=shape)
+    got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, dtype=dtype, shape=shape, exchange="rccl")
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))

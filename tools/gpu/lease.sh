@@ -136,14 +136,20 @@ for step in "$@"; do
           # variant ovl (default rounds) | serial | xcu<C> | xcu<C>x (exchange on C CUs per XCD, x: launches off them)
           IFS=':' read -r c nr ex var tr <<< "${step#xr:}"
           envs=()
-          case "$var" in
-            ovl) ;; serial) envs=(STENCIL_SLAB_SERIAL=1) ;;
-            xcu*x) cc=${var#xcu}; envs=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
-            xcu*) envs=(STENCIL_SLAB_XCU=${var#xcu}) ;;
-            *) echo "bad variant $var"; exit 2 ;;
-          esac
+          for v in ${var//+/ }; do   # variants combine with '+', e.g. nosig+xcu1x
+            case "$v" in
+              ovl) ;; serial) envs+=(STENCIL_SLAB_SERIAL=1) ;; rser) envs+=(STENCIL_SLAB_ROLLING_OVERLAP=0) ;;
+              nosig) envs+=(STENCIL_SLAB_SIGNAL=0) ;; cpwait) envs+=(STENCIL_SLAB_CPWAIT=1) ;;
+              wire*) envs+=(STENCIL_SLAB_WIRE_GBPS=${v#wire}) ;;   # emulated xGMI wire time (debug library)
+              nox) envs+=(STENCIL_SLAB_XCU=0) ;;
+              xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
+              xcu*) envs+=(STENCIL_SLAB_XCU=${v#xcu}) ;;
+              *) echo "bad variant $v"; exit 2 ;;
+            esac
+          done
           case "$c" in C5) a="--steps 16 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
           [ "$nr" != 0 ] && a="$a --rank-of $nr"
+          a="$a --allow-debug-library"
           name="xr_${c}_${nr}_${ex}_${var}${tr:+_$tr}"
           if [ "$tr" = trace ]; then
             (cd /tmp && env "${envs[@]}" TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv \
@@ -165,6 +171,8 @@ for step in "$@"; do
                -d "$O/xcdpmc_${dt}_w${w}_$ctr" -o run -- python3 "$R/tools/ab.py" --dtype "$dt" --grid "$nx" "$ny" "$nz" \
                --steps "$st" --reps 1 --launches 3 --variant STENCIL_TK_XCD=$w > "$O/xcdpmc_${dt}_w${w}_$ctr.log" 2>&1) || exit 1
           done ;;
+    cumask) /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/cumask_probe.hip -o /tmp/cumask_probe &&
+            timeout -k 10 60 /tmp/cumask_probe > "$O/cumask_probe.txt" 2>&1 ;;
     tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
              --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
