@@ -141,7 +141,8 @@ for step in "$@"; do
               ovl) ;; serial) envs+=(STENCIL_SLAB_SERIAL=1) ;; rser) envs+=(STENCIL_SLAB_ROLLING_OVERLAP=0) ;;
               nosig) envs+=(STENCIL_SLAB_SIGNAL=0) ;; cpwait) envs+=(STENCIL_SLAB_CPWAIT=1) ;;
               wire*) envs+=(STENCIL_SLAB_WIRE_GBPS=${v#wire}) ;;   # emulated xGMI wire time (debug library)
-              nox) envs+=(STENCIL_SLAB_XCU=0) ;;
+              nox) envs+=(STENCIL_SLAB_XCU=0) ;; noexcl) envs+=(STENCIL_SLAB_XCU_EXCL=0) ;;
+              sig*) envs+=(STENCIL_TK_SIG_CHUNKS=${v#sig}) ;; bsig*) envs+=(STENCIL_BOXK_SIG_CHUNKS=${v#bsig}) ;;
               xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
               xcu*) envs+=(STENCIL_SLAB_XCU=${v#xcu}) ;;
               *) echo "bad variant $v"; exit 2 ;;
@@ -162,8 +163,13 @@ for step in "$@"; do
     xcdab:*) # xcdab:<dtype>:nx:ny:nz:steps -- the strip kernel's XCD-patch tile order (STENCIL_TK_XCD=w), interleaved
           IFS=':' read -r dt nx ny nz st <<< "${step#xcdab:}"
           timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 5 --launches 3 \
-            --variant STENCIL_TK_XCD=0 --variant STENCIL_TK_XCD=2 --variant STENCIL_TK_XCD=4 --variant STENCIL_TK_XCD=8 \
-            --variant STENCIL_TK_XCD=16 > "$O/xcd_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
+            --variant STENCIL_TK_XCD=0 --variant STENCIL_TK_XCD=4 --variant STENCIL_TK_XCD=8 \
+            --variant STENCIL_TK_XCD=16 --variant STENCIL_TK_XCD=32 > "$O/xcd_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
+    envbench:*) # envbench:<NAME=V[,NAME=V]>:<cfg> -- bench.py --config cfg with those variables (debug library allowed)
+          IFS=':' read -r ev c <<< "${step#envbench:}"
+          case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+          env ${ev//,/ } timeout -k 10 400 python3 bench.py --config "$c" $a --no-cpu-baseline --allow-debug-library \
+            > "$O/envbench_${c}_${ev//[=,]/_}.json" 2>> "$O/bench.err" ;;
     xcdpmc:*) # xcdpmc:<dtype>:nx:ny:nz:steps:w -- FETCH_SIZE / WRITE_SIZE passes of that variant's launches
           IFS=':' read -r dt nx ny nz st w <<< "${step#xcdpmc:}"
           for ctr in FETCH_SIZE WRITE_SIZE; do
