@@ -366,7 +366,8 @@ int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     // profiles/r04/r04q_*, r04r_*, r04s_*.
     {
         const int64_t pitch = l.row * int64_t(elem_size(p));
-        if (pitch >= kPitchPeriod && pitch % kPitchPeriod <= kPitchNear)
+        // STENCIL_ROW_RULE=0 (debug library, the pitch scans): the raw pitch
+        if (knob("STENCIL_ROW_RULE", 1) && pitch >= kPitchPeriod && pitch % kPitchPeriod <= kPitchNear)
             l.row += (pitch < 2 * kPitchPeriod ? 128 : 2048) / int64_t(elem_size(p));
     }
     // STENCIL_ROW_PAD (debug library, experiments): extra elements per row, in

@@ -116,6 +116,20 @@ for step in "$@"; do
                    "$nx" "$ny" "$nz" "$sw" 2 | sed "s/^/pad $pad: /" >> "$O/padscan.txt" 2>> "$O/bench.err" || exit 1
                done
              done ;;
+    pitchscan:*) # pitchscan:<dtype>:<cells per plane>:<nz>:<sweeps>:<w1,w2,..> -- row-pitch scan over plane widths: each
+          # width raw (STENCIL_ROW_RULE=0), +128 B, +2 KiB, and as the product pads it; ny = cells / width
+          IFS=':' read -r dt cells nz sw widths <<< "${step#pitchscan:}"
+          es=8; [ "$dt" = fp32 ] && es=4
+          for rep in 1 2; do
+            for w in ${widths//,/ }; do
+              ny=$((cells / w))
+              for v in "STENCIL_ROW_RULE=0:0" "STENCIL_ROW_RULE=0:$((128 / es))" "STENCIL_ROW_RULE=0:$((2048 / es))" "STENCIL_ROW_RULE=1:0"; do
+                env "${v%%:*}" STENCIL_ROW_PAD="${v##*:}" timeout -k 10 200 python3 tools/time_lib.py \
+                  stencil_amd/libstencil_hip_debug.so star "$dt" "$w" "$ny" "$nz" "$sw" 2 \
+                  | sed "s/^/${v%%:*} pad ${v##*:}: /" >> "$O/pitchscan_$dt.txt" 2>> "$O/bench.err" || exit 1
+              done
+            done
+          done ;;
     loop:*) c=${step#loop:}
             timeout -k 10 300 python3 bench.py --config "$c" --exchange loopback --steps 40 --warmup 4 --no-cpu-baseline \
               > "$O/bench_${c}_loopback.json" 2>> "$O/bench.err" ;;
