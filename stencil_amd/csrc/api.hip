@@ -344,7 +344,19 @@ const char* stencil_strerror(int code) {
 const char* stencil_last_error_message(void) { return g_last_msg; }
 int stencil_last_error(void) { return g_last_code; }
 
-constexpr int64_t kPitchPeriod = 32768, kPitchNear = 256;  // bytes (stencil_layout_init's pitch rule)
+constexpr int64_t kPitchPeriod = 32768;  // bytes (stencil_layout_init's pitch rule)
+
+// The row-pitch rule (round 5): pitches of 32 KiB or more
+// whose residue r modulo 32 KiB lies in [-512, +256] B run the K-step kernels
+// 3-30 % slower; such a row is padded to residue 384 (r in [0, 256]) or by
+// 128 B (r in [-512, -128]).  Returns the bytes to add.
+int64_t pitch_pad_bytes(int64_t pitch) {
+    if (pitch < kPitchPeriod - 512) return 0;
+    const int64_t r = pitch % kPitchPeriod;
+    if (pitch >= kPitchPeriod && r <= 256) return 384 - r;
+    if (r >= kPitchPeriod - 512) return 128;
+    return 0;
+}
 
 int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     if (int rc = check_problem(prob)) return rc;
@@ -356,19 +368,17 @@ int stencil_layout_init(const stencil_problem* prob, stencil_layout* out) {
     stencil_layout l{};
     l.prob = p;
     l.row = (origin_x + p.nx + r + align - 1) / align * align;
-    // Row pitches of 32 KiB or more that sit at most 256 B above a multiple of
-    // 32 KiB run the K-step kernels 20-30 % slower: 4096-wide fp64 planes
-    // (33024 B) 1055 Gcell/s against 1360 with 128 B more, 8192-wide fp32
-    // (32896 B) 1918 against 2388 with 128 B more, 8192-wide fp64 (65792 B)
-    // 1019 against 1260 with 2 KiB more (128 B more: 997).  Such rows get 128 B
-    // below 64 KiB, 2 KiB above.  Every other measured pitch ran best unpadded
-    // (512, 2048, 3072 and 4000 wide fp64, 4096 wide fp32): DESIGN.md §9.1i,
-    // profiles/r04/r04q_*, r04r_*, r04s_*.
+    // Row pitches just below or above a multiple of 32 KiB run the K-step
+    // kernels slower (4096-wide fp64, 33024 B: 1196-1238 Gcell/s against
+    // 1246-1311 at 33152; 8160-wide fp64, 65536 B: 1063-1087 against
+    // 1171-1262 with 128 B more; 8192-wide fp32, 33024 B: 2226 against 2531 at
+    // 33152; 4000-wide fp64, 32256 B: -3 %): pitch_pad_bytes() moves such rows
+    // to a residue measured fast.  Scans of 20 widths x 2 plane heights,
+    // DESIGN.md §9.1i, profiles/r05/r05h_pitchscan_*, r05i_pitchscan_*.
     {
         const int64_t pitch = l.row * int64_t(elem_size(p));
         // STENCIL_ROW_RULE=0 (debug library, the pitch scans): the raw pitch
-        if (knob("STENCIL_ROW_RULE", 1) && pitch >= kPitchPeriod && pitch % kPitchPeriod <= kPitchNear)
-            l.row += (pitch < 2 * kPitchPeriod ? 128 : 2048) / int64_t(elem_size(p));
+        if (knob("STENCIL_ROW_RULE", 1)) l.row += pitch_pad_bytes(pitch) / int64_t(elem_size(p));
     }
     // STENCIL_ROW_PAD (debug library, experiments): extra elements per row, in
     // whole 128-B units (the row-pitch scans)

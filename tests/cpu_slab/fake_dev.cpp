@@ -215,8 +215,11 @@ struct FakeDev {
         stencil_layout l{};
         l.prob = *p;
         l.row = (origin_x + p->nx + r + align - 1) / align * align;
-        if (32768 <= l.row * es && (l.row * es) % 32768 <= 256)  // api.hip's pitch rule
-            l.row += (l.row * es < 65536 ? 128 : 2048) / es;
+        {  // api.hip's pitch rule (pitch_pad_bytes)
+            const int64_t pitch = l.row * es, r = pitch % 32768;
+            if (pitch >= 32768 - 512)
+                l.row += (pitch >= 32768 && r <= 256 ? 384 - r : r >= 32768 - 512 ? 128 : 0) / es;
+        }
         l.rows = p->ny + 2 * r;
         l.plane = l.row * l.rows;
         l.zghost = std::max<int64_t>(r, p->halo);

@@ -161,3 +161,26 @@ def test_product_library_ignores_experiment_knobs(monkeypatch):
     assert _lib.load() is prod  # documented knobs keep the product
     assert prod.stencil_plan(ctypes.byref(lay), 9, ctypes.byref(launches), ctypes.byref(kernel)) == 0
     assert launches.value == 3
+
+
+def test_row_pitch_rule():
+    """stencil_layout_init's row-pitch rule: pitches of
+    32 KiB or more within [-512, +256] B of a multiple of 32 KiB move to
+    residue 384 (from [0, 256]) or 128 B up (from [-512, -128]); every other
+    pitch is the 128-B-aligned minimum.  Every preset width is covered."""
+    from stencil_amd import _lib
+    cases = {  # (dtype, nx): row pitch in bytes
+        ("fp64", 512): 4352, ("fp64", 2048): 16640, ("fp32", 4096): 16640,  # C2, C4/C5/NS, C3: no padding
+        ("fp64", 4096): 33152,   # NS4096: 33024 (r 256) -> 33152
+        ("fp64", 4000): 32384,   # 32256 (r -512) -> +128
+        ("fp64", 4128): 33280,   # r 512: unpadded
+        ("fp64", 8160): 65920,   # 65536 (r 0) -> r 384
+        ("fp64", 8192): 65920,   # 65792 (r 256) -> r 384
+        ("fp32", 8160): 33152,   # 32896 (r 128) -> r 384
+        ("fp32", 8192): 33152,   # 33024 (r 256) -> r 384
+        ("fp64", 12288): 98688,  # 98560 (r 256) -> r 384
+    }
+    for (dt, nx), want in cases.items():
+        es = 8 if dt == "fp64" else 4
+        lay = _lib.make_layout(_lib.make_problem(dims=3, dtype=_lib.F64 if dt == "fp64" else _lib.F32, nx=nx, ny=4, nz=4))
+        assert lay.row * es == want, (dt, nx, lay.row * es, want)

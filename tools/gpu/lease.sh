@@ -179,6 +179,11 @@ for step in "$@"; do
           timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 5 --launches 3 \
             --variant STENCIL_TK_XCD=0 --variant STENCIL_TK_XCD=4 --variant STENCIL_TK_XCD=8 \
             --variant STENCIL_TK_XCD=16 --variant STENCIL_TK_XCD=32 > "$O/xcd_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
+    cfgab:*) # cfgab:<dtype>:nx:ny:nz:steps:cfg1,cfg2,.. -- strip shapes (STENCIL_TK_STRIP=cfg; 1 = default), interleaved
+          IFS=':' read -r dt nx ny nz st cfgs <<< "${step#cfgab:}"
+          vs=(); for c in ${cfgs//,/ }; do vs+=(--variant "STENCIL_TK_STRIP=$c"); done
+          timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 5 --launches 3 \
+            "${vs[@]}" > "$O/cfg_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
     envbench:*) # envbench:<NAME=V[,NAME=V]>:<cfg> -- bench.py --config cfg with those variables (debug library allowed)
           IFS=':' read -r ev c <<< "${step#envbench:}"
           case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
