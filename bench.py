@@ -161,6 +161,11 @@ def parse(argv=None):
     return args
 
 
+def _lib_forms():
+    from stencil_amd import _lib
+    return _lib.SLAB_FORMS
+
+
 def library_info() -> dict:
     """Which build of the HIP library produced the line, and every STENCIL_*
     variable set in the environment (documented knobs included)."""
@@ -665,9 +670,7 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
         parallelism = (f"z-slab x{world}, one process per GPU (torch.distributed.run) through the C-ABI rank-mode "
                        "slab job (stencil_slab_create_rank), RCCL send/recv between the ranks' slabs" +
                        (f"; ONE grid per slab + a rolling margin of {roll['margin']} planes" if roll["margin"] else ""))
-        form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
-            "serial launches (whole slab, then the exchange)" if kt.get("serial") else \
-            "boundary + interior launches"
+        form = _lib_forms()[kt["form"]]
         line = report(args, pre, spec, kname, plan["grid"], world, elapsed, kt["total_ms"] / max(1, kt["launches"]),
                       float(kt["cells_per_launch"]), res["k"], kt["launches"], parallelism,
                       rounds=form, launch_timing=f"hipEvents around rank 0's {form} of extra rounds after the timed "
@@ -749,9 +752,7 @@ def main_slab_job(args):
     else:
         check = global_grid_check(spec, plan["grid"], sweeps, sums, 0, init=args.init)
     kname = "boxk" if spec.shape == "box" else "temporalk"
-    form = "rolling passes" if kt["rolling"] else "face-signalled launches" if kt["signalled"] else \
-            "serial launches (whole slab, then the exchange)" if kt.get("serial") else \
-        "boundary + interior launches"
+    form = _lib_forms()[kt["form"]]
     if loop:
         parallelism = ("1 GPU rehearsing an interior rank" +
                        (f" of the {args.rank_of}-GPU job (its {gnz}-plane slab of the "

@@ -73,7 +73,9 @@ int stencil_last_error(void);
  * exchange's CUs too),
  * STENCIL_SLAB_TIMEOUT_MS (a slab job's deadline for any device wait,
  * default 60000: stencil_slab_set_timeout), STENCIL_SLAB_ROLLING_OVERLAP=0
- * (rolling slab rounds exchange after the pass instead of beside it). */
+ * (rolling slab rounds exchange after the pass instead of beside it),
+ * STENCIL_SLAB_STAGED=0 (slabs whose launch takes several rounds of
+ * workgroups run face-signalled rounds instead of staged ones). */
 int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */
@@ -425,7 +427,8 @@ enum {
     STENCIL_SLAB_FORM_BOUNDARY_INTERIOR = 0, /* boundary planes on one stream, the interior on another */
     STENCIL_SLAB_FORM_SIGNALLED = 1,         /* one face-signalled launch, the exchange as the faces land */
     STENCIL_SLAB_FORM_ROLLING = 2,           /* one grid + a margin: a pass of z-range launches */
-    STENCIL_SLAB_FORM_SERIAL = 3             /* one launch of the whole slab, then the exchange */
+    STENCIL_SLAB_FORM_SERIAL = 3,            /* one launch of the whole slab, then the exchange */
+    STENCIL_SLAB_FORM_STAGED = 4             /* the face quarters, then the middle beside the exchange */
 };
 int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form);
 /* Bounded-time failure.  Every wait of the job for its devices (the end of

@@ -18,11 +18,13 @@ LIB_PATH = os.path.join(_HERE, "libstencil_hip.so")
 DEBUG_LIB_PATH = os.path.join(_HERE, "libstencil_hip_debug.so")
 API_KNOBS = ("STENCIL_TK_STEPS", "STENCIL_BOX_STEPS", "STENCIL_TK_PACK", "STENCIL_BOXK_PACK", "STENCIL_SLAB_SIGNAL",
              "STENCIL_SLAB_CPWAIT", "STENCIL_SLAB_SERIAL", "STENCIL_SLAB_XCU", "STENCIL_SLAB_XCU_EXCL",
-             "STENCIL_SLAB_TIMEOUT_MS", "STENCIL_SLAB_ROLLING_OVERLAP")
+             "STENCIL_SLAB_TIMEOUT_MS", "STENCIL_SLAB_ROLLING_OVERLAP", "STENCIL_SLAB_STAGED")
 
 STENCIL_OK = 0
 ETIMEOUT = -6
-SLAB_FORMS = {0: "boundary + interior", 1: "face-signalled", 2: "rolling", 3: "serial"}
+SLAB_FORMS = {0: "boundary + interior launches", 1: "face-signalled launches", 2: "rolling passes",
+              3: "serial launches (whole slab, then the exchange)",
+              4: "staged launches (the face quarters, then the middle beside the exchange)"}
 F32, F64 = 0, 1
 STAR, BOX = 0, 1
 ORDER_NAIVE, ORDER_DMA = 0, 1

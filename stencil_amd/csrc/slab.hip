@@ -152,6 +152,9 @@ struct HipDev {
     // STENCIL_SLAB_SERIAL=1: every full round as one plain launch of the whole
     // slab followed by the exchange (no overlap)
     static bool serial_rounds() { return api_knob("STENCIL_SLAB_SERIAL", 0) != 0; }
+    // STENCIL_SLAB_STAGED=0: many-round slabs run face-signalled rounds (the
+    // exchange confined) instead of staged ones
+    static bool staged_rounds() { return api_knob("STENCIL_SLAB_STAGED", 1) != 0; }
     // STENCIL_SLAB_ROLLING_OVERLAP=0: rolling rounds exchange after the pass
     // (slab_round_rolling) instead of beside it (slab_round_rolling_overlap)
     static bool rolling_overlap() { return api_knob("STENCIL_SLAB_ROLLING_OVERLAP", 1) != 0; }

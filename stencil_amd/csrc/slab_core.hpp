@@ -108,6 +108,7 @@ struct Job {
     int position = 0;
     bool roll_overlap = false;  // rolling rounds with the exchange beside the pass (staged faces)
     bool confine = false;       // the exchange on a few CUs of its own, the launches off them
+    bool staged = false;        // full rounds: face ranges, then the middle beside the exchange
     std::vector<Slab<Dev>> s;
     // kernel timing: events around slab 0's compute launch(es) of every round
     bool timing = false;
@@ -382,6 +383,49 @@ int slab_round_signal(Job<Dev>& j, int k) {
         // this launch reads: A must also follow B
         SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
     }
+    j.chained = true;
+    j.cur_is_a = dst_pos == 0;
+    return STENCIL_OK;
+}
+
+// One STAGED round of `k` fused sweeps (the default for slabs whose launch
+// takes several rounds of workgroups, e.g. 4096^2 planes):
+//   A (stream A, every CU): the face ranges [0, F) and [n - F, n) of the new
+//     grid, F = n / 4 (at least 2K planes): half the round's work;
+//   then, beside each other, the exchange of A's faces (stream X, confined to
+//     one CU per XCD) and B (stream B, the other CUs): the middle [F, n - F).
+// B starts after A (the launches' z lock-step between neighbouring tiles
+// survives; running them concurrently broke it), and the next
+// round's A waits for B and for the exchange.  No face signals: A's end is
+// the faces' readiness.  The same kernels and sums as one launch of [0, n).
+template <class Dev>
+inline int64_t staged_face_span(const Job<Dev>& j, int64_t n) {
+    const int64_t want = std::max<int64_t>((n + 3) / 4, 2 * int64_t(j.k));
+    return std::min(want, n / 2);
+}
+
+template <class Dev>
+int slab_round_staged(Job<Dev>& j, int k) {
+    const int src_pos = cur_pos(j), dst_pos = 1 - src_pos;
+    for (size_t i = 0; i < j.s.size(); ++i) {
+        Slab<Dev>& s = j.s[i];
+        SLAB_TRY(Dev::set_device(s.device));
+        void* src = grid_at(j, s, src_pos);
+        void* dst = grid_at(j, s, dst_pos);
+        // A(r) writes planes B(r-1) read, and reads the halos exchange(r-1)
+        // received (A waits for X in exchange()'s bracket already)
+        if (j.chained) SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
+        const int64_t F = staged_face_span(j, s.n);
+        SLAB_TRY(time_begin(j, i, s.sa));
+        SLAB_TRY(Dev::sweepk(&s.l, src, dst, 0, F, k, s.sa));
+        SLAB_TRY(Dev::sweepk(&s.l, src, dst, s.n - F, s.n, k, s.sa));
+        SLAB_TRY(Dev::event_record(s.ev_bnd, s.sa));  // A done: the faces
+        SLAB_TRY(Dev::stream_wait(s.sb, s.ev_bnd));
+        if (s.n > 2 * F) SLAB_TRY(Dev::sweepk(&s.l, src, dst, F, s.n - F, k, s.sb));
+        SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, s.n > 2 * F ? 3 : 2));
+        SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
+    }
+    SLAB_TRY(exchange(j, dst_pos));  // X after A (bracket), beside B; A waits for X
     j.chained = true;
     j.cur_is_a = dst_pos == 0;
     return STENCIL_OK;
@@ -751,6 +795,12 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
             p.flags = STENCIL_HALO_LO | STENCIL_HALO_HI;
             stencil_layout l{};
             if (Dev::layout_init(&p, &l) == STENCIL_OK) j->confine = Dev::confine_exchange(l, j->k);
+            // such grids run STAGED rounds by default (below): the face ranges
+            // first, then the middle, the exchange beside the middle
+            if (j->confine && Dev::staged_rounds()) {
+                j->staged = true;
+                j->signal = false;
+            }
         }
     }
     j->timeout_ms = Dev::default_timeout_ms();
@@ -797,7 +847,10 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         } else {
             if ((rc = Dev::alloc(s.l.bytes + 256, &s.a)) || (rc = Dev::alloc(s.l.bytes + 256, &s.b))) break;
         }
-        if ((rc = Dev::stream_create(&s.sa, STREAM_BOUNDARY, j->confine)) ||
+        // staged rounds: the face launches (A) take every CU -- nothing runs
+        // beside them -- and only the middle launch (B) and the exchange are
+        // confined
+        if ((rc = Dev::stream_create(&s.sa, STREAM_BOUNDARY, j->confine && !j->staged)) ||
             (rc = Dev::stream_create(&s.sb, STREAM_INTERIOR, j->confine)) ||
             (rc = Dev::stream_create(&s.sx, STREAM_EXCHANGE, j->confine)) || (rc = Dev::event_create(&s.ev_bnd, false)) ||
             (rc = Dev::event_create(&s.ev_int, false)) || (rc = Dev::event_create(&s.ev_join, false)) ||
@@ -1058,6 +1111,8 @@ int one_round(Job<Dev>& j, int k, bool full) {
         SLAB_FAIL(j, j.roll_overlap ? slab_round_rolling_overlap(j, k) : slab_round_rolling(j, k));
     else if (full && j.signal)
         SLAB_FAIL(j, slab_round_signal(j, k));
+    else if (full && j.staged)
+        SLAB_FAIL(j, slab_round_staged(j, k));
     else
         SLAB_FAIL(j, slab_round(j, k));
     SLAB_FAIL(j, mark_round(j));
@@ -1123,6 +1178,7 @@ int kernel_timing(JobT* job, int32_t enable) {
 template <class Dev>
 int round_form_of(const Job<Dev>& j) {
     return j.signal ? STENCIL_SLAB_FORM_SIGNALLED
+           : j.staged ? STENCIL_SLAB_FORM_STAGED
            : j.margin ? STENCIL_SLAB_FORM_ROLLING
            : j.serial ? STENCIL_SLAB_FORM_SERIAL
                       : STENCIL_SLAB_FORM_BOUNDARY_INTERIOR;

@@ -237,7 +237,16 @@ struct FakeDev {
         return p.dtype == STENCIL_F32 && p.nx * p.ny >= (int64_t(1) << 20) ? 5 : 4;
     }
     static bool signal_enabled() { return fake::g_signal; }
-    static bool confine_exchange(const stencil_layout&, int) { return false; }  // the fake has no CUs
+    // the fake has no CUs: FAKE_SLAB_CONFINE=1 treats every slab as a grid of
+    // several rounds of workgroups (staged rounds, unless STENCIL_SLAB_STAGED=0)
+    static bool confine_exchange(const stencil_layout&, int) {
+        const char* v = std::getenv("FAKE_SLAB_CONFINE");
+        return v && std::atoi(v) != 0;
+    }
+    static bool staged_rounds() {
+        const char* v = std::getenv("STENCIL_SLAB_STAGED");
+        return !(v && *v && std::atoi(v) == 0);
+    }
     static int wire_delay(Stream, size_t) { return STENCIL_OK; }
     static int free_bytes(int64_t* out) {
         *out = fake::g_free;

@@ -483,7 +483,31 @@ def test_many_round_signalled_launch_face_chunks_first(gpu, monkeypatch, shape, 
     confine the exchange to one CU per XCD, STENCIL_SLAB_XCU): bitwise the
     boundary + interior rounds."""
     monkeypatch.setenv("STENCIL_SLAB_XCU", xcu)
+    monkeypatch.setenv("STENCIL_SLAB_STAGED", "0")  # face signals, not the staged rounds AUTO runs here
     nx, ny, nz, it = 2048, 1024, 40, 9
     want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape=shape)
     got = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, True, dtype=dtype, shape=shape, exchange="rccl")
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+@pytest.mark.parametrize("shape", ["star", "box"])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("exchange", ["rccl", "copy"])
+def test_staged_rounds_match_boundary_launches(gpu, monkeypatch, shape, dtype, exchange):
+    """STAGED rounds, AUTO's form for slabs whose launch takes several rounds
+    of workgroups (2048 x 1024 planes): the face quarters on every CU, then
+    the middle on the CUs the confined exchange leaves; remainders after the
+    full rounds -- bitwise the boundary + interior rounds."""
+    nx, ny, nz, it = 2048, 1024, 44, 11
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape=shape)
+    monkeypatch.delenv("STENCIL_SLAB_SIGNAL", raising=False)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    job = SlabJob(spec, nx, ny, nz, [gpu], exchange=exchange, periodic=True)
+    try:
+        assert job.round_form() == 4
+        job.fill_initial("random", 5)
+        job.run(it)
+        got = job.download()
+    finally:
+        job.close()
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))

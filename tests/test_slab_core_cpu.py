@@ -386,3 +386,59 @@ def test_fake_layout_is_the_product_layout(fake, dtype):
             want, got = _lib.make_layout(prob), fake.layout(prob)
             for f, _ in _lib.Layout._fields_[1:]:
                 assert getattr(got, f) == getattr(want, f), (nx, r, halo, f)
+
+
+@pytest.mark.parametrize("dtype,shape,k", SHAPES)
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("exchange", ["rccl", "copy"])
+def test_staged_rounds_equal_one_grid(fake, monkeypatch, dtype, shape, k, nslabs, exchange):
+    """STAGED rounds (the default for slabs whose launch takes several rounds
+    of workgroups; FAKE_SLAB_CONFINE=1 makes the fake's slabs such): per full
+    round the two face quarters, then the middle, the exchange beside it;
+    remainder rounds and continued calls; bitwise one grid."""
+    monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
+    nx, ny, nz = 13, 7, 10 * k * nslabs + 3
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange=exchange, lib=fake)
+    assert job.round_form() == 4
+    job.fill_initial("random", 11)
+    sweeps = 0
+    for it in (2 * k + 1, k, 1, k - 1):
+        fake.stats(reset=True)
+        job.run(it)
+        sweeps += it
+        st = fake.stats()
+        assert st["signal_sweeps"] == 0
+        full, rem = it // k, it % k
+        # 3 launches per slab and full round (face quarters + middle); a remainder round: boundary + interior (3)
+        assert st["sweeps"] == 3 * nslabs * (full + (1 if rem else 0)), st
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps))
+    job.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_staged_rank_mode_equals_one_grid(fake, monkeypatch, nranks):
+    monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
+    k = 4
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 10, 6, 12 * nranks + 1
+    sweeps = 3 * k + 2
+
+    def fn(job, r):
+        assert job.round_form() == 4
+        job.fill_initial("random", 21)
+        job.run(sweeps)
+        return job.info(0), job.download()
+
+    out, errs = _rank_jobs(fake, spec, (nx, ny, nz), nranks, fn)
+    assert not any(errs), errs
+    want = oracle_grid(spec, nx, ny, nz, sweeps, seed=21)
+    got = np.zeros_like(want)
+    for r in range(nranks):
+        inf, dense = out[r]
+        z0 = inf["first"] + (0 if r > 0 else -1)
+        z1 = inf["first"] + inf["planes"] + (1 if r == nranks - 1 else 0)
+        got[z0 + 1:z1 + 1] = dense[z0 + 1:z1 + 1]
+    assert_bitwise(got, want)
