@@ -286,6 +286,7 @@ def _periodic_job(gpu, monkeypatch, nx, ny, nz, it, signalled, dtype="fp64", sha
     interior rank's rounds), face-signalled or boundary + interior rounds
     (STENCIL_SLAB_SIGNAL), halos by device copies or RCCL to itself."""
     monkeypatch.setenv("STENCIL_SLAB_SIGNAL", "1" if signalled else "0")
+    monkeypatch.setenv("STENCIL_SLAB_STAGED", "0")  # many-round planes: signals, not AUTO's staged rounds
     spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
     job = SlabJob(spec, nx, ny, nz, [gpu], exchange=exchange, periodic=True)
     try:
@@ -501,6 +502,7 @@ def test_staged_rounds_match_boundary_launches(gpu, monkeypatch, shape, dtype, e
     nx, ny, nz, it = 2048, 1024, 44, 11
     want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape=shape)
     monkeypatch.delenv("STENCIL_SLAB_SIGNAL", raising=False)
+    monkeypatch.delenv("STENCIL_SLAB_STAGED", raising=False)
     spec = StencilSpec(dims=3, dtype=dtype, shape=shape)
     job = SlabJob(spec, nx, ny, nz, [gpu], exchange=exchange, periodic=True)
     try:
