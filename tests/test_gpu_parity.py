@@ -995,8 +995,9 @@ def test_padded_row_pitch_matches_oracle(gpu, dtype, nx):
     launches on such a layout stay bitwise the oracle."""
     e = engine(gpu, 3, dtype, "star", 1, "naive", "auto", nx, 20, 14)
     es = 8 if dtype == "fp64" else 4
-    r = (e.layout.row * es) % 32768
-    assert 256 < r < 32768 - 512, e.layout.row  # the rule applied
+    align = 128 // es
+    raw = (align + nx + 1 + align - 1) // align * align  # the 128-B-aligned minimum row (r = 1)
+    assert e.layout.row > raw, e.layout.row  # the rule applied
     e.reset("random", 21)
     fin, _ = e.iterate(9)
     p = ob.problem(3, dtype, "star", 1, "naive", nx, 20, 14)
