@@ -87,6 +87,10 @@ struct Slab {
     // the halo slots after the pass (2 x depth planes each: lo face, hi face)
     void* xs = nullptr;
     void* xr = nullptr;
+    // staged rounds: the face span F (0 = the default n / 4 until tuned) and
+    // the timing events of the tuning rounds (B on its stream, the exchange)
+    int64_t face_span = 0;
+    typename Dev::Event tb0{}, tb1{}, tx0{}, tx1{};
 };
 
 template <class Dev>
@@ -109,6 +113,8 @@ struct Job {
     bool roll_overlap = false;  // rolling rounds with the exchange beside the pass (staged faces)
     bool confine = false;       // the exchange on a few CUs of its own, the launches off them
     bool staged = false;        // full rounds: face ranges, then the middle beside the exchange
+    int tune_left = 2;          // staged: timed rounds left before the face span is set
+    bool tuning = false;        // this round records the tuning events
     std::vector<Slab<Dev>> s;
     // kernel timing: events around slab 0's compute launch(es) of every round
     bool timing = false;
@@ -227,6 +233,7 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
         SLAB_TRY(Dev::event_record(s.ev_xin, s.sa));
         SLAB_TRY(Dev::stream_wait(s.sx, s.ev_xin));
         SLAB_TRY(pre(s));
+        if (j.tuning) SLAB_TRY(Dev::event_record(s.tx0, s.sx));
         // tests / rehearsals: the transfer's wire time between distinct GPUs (a no-op unless asked for)
         SLAB_TRY(Dev::wire_delay(s.sx, size_t(d) * plane_bytes(s)));
         SLAB_TRY(Dev::event_record(s.ev_join, s.sx));  // this slab's faces are ready
@@ -275,6 +282,7 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
     }
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
+        if (j.tuning) SLAB_TRY(Dev::event_record(s.tx1, s.sx));
         SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
     }
     for (int i = 0; i < n; ++i) {
@@ -399,9 +407,27 @@ int slab_round_signal(Job<Dev>& j, int k) {
 // round's A waits for B and for the exchange.  No face signals: A's end is
 // the faces' readiness.  The same kernels and sums as one launch of [0, n).
 template <class Dev>
-inline int64_t staged_face_span(const Job<Dev>& j, int64_t n) {
-    const int64_t want = std::max<int64_t>((n + 3) / 4, 2 * int64_t(j.k));
-    return std::min(want, n / 2);
+inline int64_t staged_face_span(const Job<Dev>& j, const Slab<Dev>& s) {
+    if (s.face_span > 0) return s.face_span;
+    const int64_t want = std::max<int64_t>((s.n + 3) / 4, 2 * int64_t(j.k));
+    return std::min(want, s.n / 2);
+}
+
+// The face span after the tuning rounds: B (the middle, beside the exchange)
+// is kept 1.25x as long as the measured exchange and no longer, within
+// [n / 4, n / 2 - 2K] -- the more of the round's work A does on every CU, the
+// less runs on the 248 CUs the confined exchange leaves.  In a rehearsal the
+// exchange is a local copy on the confined CUs (NS4096 rank of 4: 9 ms); over
+// xGMI it is the wire time.
+template <class Dev>
+int64_t tuned_face_span(const Job<Dev>& j, const Slab<Dev>& s, float b_ms, float x_ms) {
+    const int64_t F = staged_face_span(j, s), mid = s.n - 2 * F;
+    const int64_t lo = std::min<int64_t>(std::max<int64_t>((s.n + 3) / 4, 2 * int64_t(j.k)), s.n / 2);
+    const int64_t hi = std::max<int64_t>(lo, s.n / 2 - 2 * int64_t(j.k));
+    if (mid <= 0 || b_ms <= 0.f) return lo;
+    const double per_plane = double(b_ms) / double(mid);
+    const int64_t need = int64_t(1.25 * double(x_ms) / per_plane) + 1;
+    return std::max(lo, std::min(hi, (s.n - need) / 2));
 }
 
 template <class Dev>
@@ -415,13 +441,15 @@ int slab_round_staged(Job<Dev>& j, int k) {
         // A(r) writes planes B(r-1) read, and reads the halos exchange(r-1)
         // received (A waits for X in exchange()'s bracket already)
         if (j.chained) SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
-        const int64_t F = staged_face_span(j, s.n);
+        const int64_t F = staged_face_span(j, s);
         SLAB_TRY(time_begin(j, i, s.sa));
         SLAB_TRY(Dev::sweepk(&s.l, src, dst, 0, F, k, s.sa));
         SLAB_TRY(Dev::sweepk(&s.l, src, dst, s.n - F, s.n, k, s.sa));
         SLAB_TRY(Dev::event_record(s.ev_bnd, s.sa));  // A done: the faces
         SLAB_TRY(Dev::stream_wait(s.sb, s.ev_bnd));
+        if (j.tuning) SLAB_TRY(Dev::event_record(s.tb0, s.sb));
         if (s.n > 2 * F) SLAB_TRY(Dev::sweepk(&s.l, src, dst, F, s.n - F, k, s.sb));
+        if (j.tuning) SLAB_TRY(Dev::event_record(s.tb1, s.sb));
         SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, s.n > 2 * F ? 3 : 2));
         SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
     }
@@ -714,7 +742,7 @@ void release(JobT* j) {
             if (p) Dev::free(p);
         for (typename Dev::Stream st : {s.sx, s.sa, s.sb})
             if (st) Dev::stream_destroy(st);
-        for (typename Dev::Event e : {s.ev_bnd, s.ev_int, s.ev_join, s.ev_xin, s.ev_xout})
+        for (typename Dev::Event e : {s.ev_bnd, s.ev_int, s.ev_join, s.ev_xin, s.ev_xout, s.tb0, s.tb1, s.tx0, s.tx1})
             if (e) Dev::event_destroy(e);
         for (typename Dev::Event e : s.ring)
             if (e) Dev::event_destroy(e);
@@ -856,6 +884,10 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
             (rc = Dev::event_create(&s.ev_int, false)) || (rc = Dev::event_create(&s.ev_join, false)) ||
             (rc = Dev::event_create(&s.ev_xin, false)) || (rc = Dev::event_create(&s.ev_xout, false)))
             break;
+        if (j->staged)
+            for (auto* e : {&s.tb0, &s.tb1, &s.tx0, &s.tx1})
+                if ((rc = Dev::event_create(e, true))) break;
+        if (rc) break;
         s.ring.assign(size_t(kInflight), typename Dev::Event{});
         for (auto& e : s.ring)
             if ((rc = Dev::event_create(&e, false))) break;
@@ -1111,8 +1143,24 @@ int one_round(Job<Dev>& j, int k, bool full) {
         SLAB_FAIL(j, j.roll_overlap ? slab_round_rolling_overlap(j, k) : slab_round_rolling(j, k));
     else if (full && j.signal)
         SLAB_FAIL(j, slab_round_signal(j, k));
-    else if (full && j.staged)
+    else if (full && j.staged) {
+        // the first two staged rounds are timed (the first also carries
+        // RCCL's lazy connection set-up): the second sets the face span
+        j.tuning = j.tune_left > 0;
         SLAB_FAIL(j, slab_round_staged(j, k));
+        if (j.tuning) {
+            j.tuning = false;
+            SLAB_TRY(sync_bounded(j));
+            if (--j.tune_left == 0)
+                for (Slab<Dev>& s : j.s) {
+                    SLAB_FAIL(j, Dev::set_device(s.device));
+                    float b_ms = 0.f, x_ms = 0.f;
+                    SLAB_FAIL(j, Dev::event_elapsed(&b_ms, s.tb0, s.tb1));
+                    SLAB_FAIL(j, Dev::event_elapsed(&x_ms, s.tx0, s.tx1));
+                    s.face_span = tuned_face_span(j, s, b_ms, x_ms);
+                }
+        }
+    }
     else
         SLAB_FAIL(j, slab_round(j, k));
     SLAB_FAIL(j, mark_round(j));
