@@ -10,7 +10,8 @@ exactly its 1000 iterations).  At N>1 every rank owns a 512^3 Z-slab of a
 512 x 512 x 512N grid (weak scaling) and exchanges K halo planes with each
 neighbour per round of K fused sweeps (K = 4: the strip-layout K-step
 kernel) over RCCL, overlapped with the rest of the round's launch
-(face-signalled rounds, csrc/slab_core.hpp).
+(face-signalled rounds on such few-tile planes; staged rounds on wide ones;
+csrc/slab_core.hpp).
 
 Multi-GPU drivers, same job, same JSON line, ONE implementation of the rounds
 (the C-ABI slab job, csrc/slab_core.hpp):

@@ -416,7 +416,8 @@ int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
  * z-range launches in rolling rounds) on that launch's stream.  kernel_time
  * synchronises and returns the summed device time, the spans timed, the
  * interior cells one span covers and whether the rounds are face-signalled
- * (1) or not (0); stencil_slab_round_form gives the form.  Enabling (or
+ * (1) or not (0); stencil_slab_round_form gives the form (a staged round's
+ * span is its face launches and its middle launch).  Enabling (or
  * disabling) drops earlier records. */
 int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
 int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,

@@ -462,7 +462,7 @@ class SlabJob:
                 "signalled": int(sig.value) == 1, "rolling": form == 2, "serial": form == 3, "form": form}
 
     def round_form(self) -> int:
-        """0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial."""
+        """0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial, 4 staged."""
         f = ctypes.c_int32(-1)
         _lib.check(self.lib.stencil_slab_round_form(self.job, ctypes.byref(f)), "stencil_slab_round_form", lib=self.lib)
         return int(f.value)
