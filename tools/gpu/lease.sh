@@ -185,6 +185,11 @@ for step in "$@"; do
           vs=(); for c in ${cfgs//,/ }; do vs+=(--variant "STENCIL_TK_STRIP=$c"); done
           timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 5 --launches 3 \
             "${vs[@]}" > "$O/cfg_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
+    kab:*) # kab:<dtype>:nx:ny:nz -- fp32 K = 5 (default) against K = 4 shapes, interleaved (debug library)
+          IFS=':' read -r dt nx ny nz <<< "${step#kab:}"
+          timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps 5 --reps 5 --launches 3 \
+            --variant STENCIL_TK_STRIP=1 --variant STEPS=4,STENCIL_TK_STRIP=1,NOCHECK=1 --variant STEPS=4,STENCIL_TK_STRIP=20808,NOCHECK=1 \
+            --variant STEPS=4,STENCIL_TK_STRIP=20808,STENCIL_TK_XCD=0,NOCHECK=1 > "$O/k_ab_${dt}_${nx}x${ny}x${nz}.txt" 2>&1 ;;
     envbench:*) # envbench:<NAME=V[,NAME=V]>:<cfg> -- bench.py --config cfg with those variables (debug library allowed)
           IFS=':' read -r ev c <<< "${step#envbench:}"
           case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
