@@ -161,6 +161,10 @@ struct HipDev {
     // STENCIL_SLAB_NO_PULL_WAIT=1 (debug library, the test that shows the
     // delay below exposing the race): drop the rolling exchange's wait
     static bool pull_wait_enabled() { return knob("STENCIL_SLAB_NO_PULL_WAIT", 0) == 0; }
+    // STENCIL_SLAB_SIG_SKEW=n (debug library, the bounded-failure test): the
+    // first face-signalled round waits for n face adds more than its launch
+    // makes, so its face wait only ends when the job's deadline releases it
+    static int debug_signal_skew() { return std::max(0, knob("STENCIL_SLAB_SIG_SKEW", 0)); }
     // STENCIL_SLAB_COPY_DELAY_US (debug library, tests): a one-lane spin of
     // that many microseconds queued before slab 0 pulls its neighbours' faces
     // (the others run on), so that a missing stream dependency of the copy

@@ -377,6 +377,7 @@ int slab_round_signal(Job<Dev>& j, int k) {
         SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, 1));
         SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
         s.sig_target += uint32_t(nsig);
+        if (j.rounds == 0) s.sig_target += uint32_t(Dev::debug_signal_skew());  // tests: a face wait that never ends
         if (s.fsig) s.fsig_target += 2;  // both faces of this launch: +2
     }
     // the wait for the faces goes first on the exchange stream
@@ -653,13 +654,18 @@ template <class Dev>
 int fail(Job<Dev>& j, int rc) {
     if (rc == STENCIL_OK || j.failed) return rc;
     j.failed = rc;
+    // the waits first: RCCL's kernels may be queued behind them, and an
+    // abort that waited for those would wait for the waits
+    for (Slab<Dev>& s : j.s) {
+        (void)Dev::set_device(s.device);
+        Dev::release_waits(s.tflag, s.fsig);
+    }
     for (Slab<Dev>& s : j.s) {
         (void)Dev::set_device(s.device);
         if (s.comm) {
             Dev::comm_abort(s.comm);
             s.comm = typename Dev::Comm{};
         }
-        Dev::release_waits(s.tflag, s.fsig);
     }
     return rc;
 }

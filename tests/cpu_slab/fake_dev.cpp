@@ -302,6 +302,7 @@ struct FakeDev {
     static int stream_wait(Stream, Event) { return STENCIL_OK; }
     static int debug_delay(Stream, int) { return STENCIL_OK; }  // copies are synchronous here
     static bool pull_wait_enabled() { return true; }
+    static int debug_signal_skew() { return 0; }
     static int event_elapsed(float* ms, Event a, Event b) {
         *ms = std::chrono::duration<float, std::milli>(b->t - a->t).count();
         return STENCIL_OK;

@@ -513,3 +513,35 @@ def test_staged_rounds_match_boundary_launches(gpu, monkeypatch, shape, dtype, e
     finally:
         job.close()
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+def test_face_wait_past_the_deadline_fails_the_job_in_time(gpu, monkeypatch):
+    """Bounded-time failure on the HIP path: the first
+    face-signalled round waits for more face adds than its launch makes
+    (STENCIL_SLAB_SIG_SKEW, debug library), as if a face never came.  With a
+    1.5 s job deadline, run() returns STENCIL_ETIMEOUT after about that long --
+    the host released the polling wait through its host-coherent flag, well
+    before the kernel's own 10 s give-up -- later calls fail at once, and
+    destroy returns."""
+    import time
+    from stencil_amd import _lib
+    monkeypatch.setenv("STENCIL_SLAB_SIGNAL", "1")
+    monkeypatch.setenv("STENCIL_SLAB_SIG_SKEW", "1000")
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 130, 64, 20, [gpu], exchange="rccl", periodic=True)
+    try:
+        assert job.round_form() == 1
+        job.set_timeout(1500)
+        job.fill_initial("random", 5)
+        t0 = time.monotonic()
+        with pytest.raises(_lib.StencilError) as ei:
+            job.run(8)
+        took = time.monotonic() - t0
+        assert ei.value.code == _lib.ETIMEOUT, ei.value
+        assert took < 6.0, took
+        with pytest.raises(_lib.StencilError, match="failed earlier"):
+            job.run(4)
+    finally:
+        t1 = time.monotonic()
+        job.close()
+        assert time.monotonic() - t1 < 15.0
