@@ -719,7 +719,9 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         // (the exchange's kernels run beside the launch), faces in the first
         // round's chunks, and no timing trial (its extra launches would add to
         // the face counters the exchange waits on): the model's choice
-        const int pslots = SIG ? slots - slots / 32 : slots;
+        // STENCIL_TK_SIG_SPARE (debug library): CUs per XCD the packed
+        // face-signalled schedule leaves to the exchange (default 1)
+        const int pslots = SIG ? slots - slots / 32 * senv_int("STENCIL_TK_SIG_SPARE", 1) : slots;
         const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, pslots, zc, s,
                                        tl_dry_launch != nullptr, &sched, &nb, &verdict, SIG);
         if (rc != STENCIL_OK) return rc;
