@@ -377,7 +377,10 @@ int stencil_slab_create2(const stencil_problem* global, int32_t ngpus, const int
  * rank by its own channel (a torch.distributed broadcast, MPI_Bcast, a file);
  * each rank then calls stencil_slab_create_rank with the same global problem
  * and builds only its slab (z split as above, slab = rank) on `device`, joined
- * by ncclCommInitRank -- a collective: every rank must call it.  The job then
+ * by ncclCommInitRank -- a collective: every rank must call it (a rank that
+ * does not within STENCIL_SLAB_TIMEOUT_MS fails the others' calls with
+ * STENCIL_ETIMEOUT; RCCL's bootstrap thread for the abandoned attempt then
+ * stays blocked until the process exits).  The job then
  * holds ONE slab (stencil_slab_info slab 0) and every call below is
  * per-rank and collective over the ranks (run: every rank the same
  * iterations).  Host arrays keep the global shape: upload reads and download /

@@ -20,9 +20,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -376,12 +378,62 @@ struct HipDev {
         if (e != ncclSuccess) return set_error(STENCIL_EHIP, "ncclCommInitAll(%d) failed: %s", n, rccl().GetErrorString(e));
         return STENCIL_OK;
     }
-    static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank) {
+    // ncclCommInitRank is a collective: it returns once every rank of the id
+    // has joined, and waits for a missing rank forever.  It runs on a helper
+    // thread (on the caller's device) and the caller waits at most
+    // `timeout_ms`; past that it gets STENCIL_ETIMEOUT and the helper is left
+    // behind, blocked in RCCL's bootstrap -- it destroys the communicator
+    // itself should the missing ranks join after all (nobody else holds it).
+    // A nonblocking communicator could be aborted instead, but its every
+    // group end returns before RCCL's kernels are queued, which the rounds'
+    // event brackets on the exchange stream cannot allow.
+    struct InitCall {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclComm_t comm = nullptr;
+        ncclResult_t res = ncclSuccess;
+        bool device_ok = true;
+    };
+    static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank, int64_t timeout_ms) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        const ncclResult_t e = rccl().CommInitRank(comm, nranks, u, rank);
-        if (e != ncclSuccess)
-            return set_error(STENCIL_EHIP, "ncclCommInitRank(%d of %d) failed: %s", rank, nranks, rccl().GetErrorString(e));
+        int dev = 0;
+        STENCIL_HIP_CHECK(hipGetDevice(&dev));
+        auto call = std::make_shared<InitCall>();
+        try {
+            std::thread([call, u, nranks, rank, dev] {
+                ncclComm_t c = nullptr;
+                ncclResult_t r = ncclSuccess;
+                const bool dok = hipSetDevice(dev) == hipSuccess;
+                if (dok) r = rccl().CommInitRank(&c, nranks, u, rank);
+                std::lock_guard<std::mutex> lk(call->mu);
+                if (call->abandoned) {
+                    if (dok && r == ncclSuccess && c) (void)rccl().CommDestroy(c);
+                    return;
+                }
+                call->comm = c;
+                call->res = r;
+                call->device_ok = dok;
+                call->done = true;
+                call->cv.notify_all();
+            }).detach();
+        } catch (const std::exception& e) {
+            return set_error(STENCIL_EHIP, "communicator creation: no helper thread (%s)", e.what());
+        }
+        std::unique_lock<std::mutex> lk(call->mu);
+        if (!call->cv.wait_for(lk, std::chrono::milliseconds(std::max<int64_t>(1, timeout_ms)),
+                               [&] { return call->done; })) {
+            call->abandoned = true;
+            return set_error(STENCIL_ETIMEOUT,
+                             "ncclCommInitRank(rank %d of %d): not every rank joined within %lld ms "
+                             "(STENCIL_SLAB_TIMEOUT_MS)", rank, nranks, (long long)timeout_ms);
+        }
+        if (!call->device_ok) return set_error(STENCIL_EHIP, "communicator creation: hipSetDevice(%d) failed", dev);
+        if (call->res != ncclSuccess)
+            return set_error(STENCIL_EHIP, "ncclCommInitRank(%d of %d) failed: %s", rank, nranks,
+                             rccl().GetErrorString(call->res));
+        *comm = call->comm;
         return STENCIL_OK;
     }
     static void comm_destroy(Comm c) {

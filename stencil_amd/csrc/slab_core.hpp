@@ -982,9 +982,11 @@ int create_rank(const stencil_problem* global, int32_t nranks, int32_t rank, int
         return rc;
     }
     // collective over the ranks: every rank must reach it (build_job's
-    // checks that depend on the global problem fail on every rank alike)
+    // checks that depend on the global problem fail on every rank alike); a
+    // rank that never arrives fails it with STENCIL_ETIMEOUT after the job's
+    // deadline
     typename Dev::Comm comm{};
-    if (int rc = Dev::comm_init_rank(&comm, nranks, id, rank)) {
+    if (int rc = Dev::comm_init_rank(&comm, nranks, id, rank, j->timeout_ms)) {
         release<Dev>(j);
         return rc;
     }

@@ -477,14 +477,17 @@ struct FakeDev {
         for (int i = 0; i < n; ++i) comms[i] = new fake::Comm{id, i, n};
         return STENCIL_OK;
     }
-    static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank) {
+    // as HipDev: a rank that never joins fails the collective with STENCIL_ETIMEOUT after timeout_ms
+    static int comm_init_rank(Comm* comm, int nranks, const void* id, int rank, int64_t timeout_ms) {
         const std::string key(static_cast<const char*>(id), STENCIL_SLAB_ID_BYTES);
         if (fake::mail_dir()) {  // ranks in separate processes: a join file each, wait for all
             const std::string base = std::string(fake::mail_dir()) + "/join_" + fake::hex_of(key) + "_";
             std::ofstream(base + std::to_string(rank)) << rank;
             for (int r = 0; r < nranks; ++r)
                 for (int it = 0; access((base + std::to_string(r)).c_str(), F_OK) != 0; ++it) {
-                    if (it > 30000) return set_error(STENCIL_EHIP, "fake comm init: rank %d never joined", r);
+                    if (it > timeout_ms)
+                        return set_error(STENCIL_ETIMEOUT, "fake comm init: rank %d did not join within %lld ms", r,
+                                         (long long)timeout_ms);
                     std::this_thread::sleep_for(std::chrono::milliseconds(1));
                 }
             *comm = new fake::Comm{key, rank, nranks};
@@ -495,8 +498,9 @@ struct FakeDev {
         ++m.joined[key];
         m.cv.notify_all();
         // a collective, as ncclCommInitRank: every rank of the id must arrive
-        if (!m.cv.wait_for(lk, std::chrono::seconds(20), [&] { return m.joined[key] >= nranks; }))
-            return set_error(STENCIL_EHIP, "fake comm init: %d of %d ranks joined", m.joined[key], nranks);
+        if (!m.cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return m.joined[key] >= nranks; }))
+            return set_error(STENCIL_ETIMEOUT, "fake comm init: %d of %d ranks joined within %lld ms", m.joined[key],
+                             nranks, (long long)timeout_ms);
         *comm = new fake::Comm{key, rank, nranks};
         return STENCIL_OK;
     }

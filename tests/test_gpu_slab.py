@@ -545,3 +545,39 @@ def test_face_wait_past_the_deadline_fails_the_job_in_time(gpu, monkeypatch):
         t1 = time.monotonic()
         job.close()
         assert time.monotonic() - t1 < 15.0
+
+
+def test_missing_rank_fails_communicator_creation_in_time(gpu):
+    """Communicator creation (stencil_slab_create_rank) is a collective: rank
+    0 of 2 whose peer never arrives gets STENCIL_ETIMEOUT after the job's
+    deadline (STENCIL_SLAB_TIMEOUT_MS) instead of blocking in RCCL's bootstrap
+    forever.  In a child process: the abandoned helper thread stays blocked
+    in the bootstrap until that process exits (slab.hip, HipDev::comm_init_rank)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import json, time\n"
+        "from stencil_amd import _lib\n"
+        "from stencil_amd.engine import SlabJob, StencilSpec\n"
+        "spec = StencilSpec(dims=3, dtype='fp64', shape='star')\n"
+        "uid = SlabJob.unique_id()\n"
+        "t0 = time.monotonic()\n"
+        "try:\n"
+        f"    SlabJob(spec, 64, 64, 32, [{int(gpu)}], rank=(2, 0, uid)).close()\n"
+        "    print(json.dumps({'code': 0, 'took': time.monotonic() - t0}))\n"
+        "except _lib.StencilError as e:\n"
+        "    print(json.dumps({'code': e.code, 'took': time.monotonic() - t0, 'msg': str(e)}))\n"
+    )
+    env = dict(os.environ, STENCIL_SLAB_TIMEOUT_MS="2000")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=90)
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["code"] == _lib.ETIMEOUT, res
+    assert 1.5 < res["took"] < 10.0, res
+    assert "not every rank joined" in res["msg"], res
+    assert time.monotonic() - t0 < 60.0

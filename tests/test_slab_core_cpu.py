@@ -322,6 +322,38 @@ def test_silent_peer_fails_every_rank_in_bounded_time(fake, monkeypatch, nranks,
         assert again[0] == _lib.ETIMEOUT and "failed earlier" in again[1], again
 
 
+@pytest.mark.parametrize("present", [1, 2])
+def test_missing_rank_fails_creation_in_bounded_time(fake, monkeypatch, present):
+    """Communicator creation is a collective: with a rank that never calls
+    stencil_slab_create_rank, the ranks that did get STENCIL_ETIMEOUT after
+    STENCIL_SLAB_TIMEOUT_MS instead of waiting for it forever."""
+    import time
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    monkeypatch.setenv("STENCIL_SLAB_TIMEOUT_MS", "600")
+    nranks = present + 1
+    uid = SlabJob.unique_id(lib=fake)
+    res = [None] * present
+
+    def body(r):
+        t0 = time.monotonic()
+        try:
+            SlabJob(spec, 8, 6, 8 * nranks, [r], rank=(nranks, r, uid), lib=fake).close()
+            res[r] = ("created", time.monotonic() - t0)
+        except _lib.StencilError as exc:
+            res[r] = (exc.code, time.monotonic() - t0, str(exc))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(present)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30)
+    assert not any(t.is_alive() for t in th), "a rank hung in creation"
+    for r in range(present):
+        assert res[r][0] == _lib.ETIMEOUT, res
+        assert 0.5 < res[r][1] < 5.0, res
+
+
 def test_upload_checks_the_rolling_ghost_ring(fake):
     """ROLLING slabs need the same x/y ghost ring in every plane:
     upload refuses a host grid whose ring varies with z, and takes it for a
