@@ -602,11 +602,12 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
         job.kernel_timing(True)
         job.run(extra)
         kt = job.kernel_time()
+        xt = job.exchange_time()
         job.kernel_timing(False)
         sweeps += extra
         sums = None if args.no_check else job.plane_sums()[info["first"]:info["first"] + info["planes"]].copy()
-        return {"info": info, "rolling": roll, "k": k, "elapsed": elapsed, "kt": kt, "sweeps": sweeps, "sums": sums,
-                "settle": settled}
+        return {"info": info, "rolling": roll, "k": k, "elapsed": elapsed, "kt": kt, "xt": xt, "sweeps": sweeps,
+                "sums": sums, "settle": settled}
     finally:
         job.close()
 
@@ -649,6 +650,13 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
         t = torch.tensor([res["elapsed"]], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # every rank's exchange times (its transfers over RCCL, and how much of
+        # them ran beside its own launches) for the line
+        xrow = torch.tensor([res["xt"]["transfer_ms"], res["xt"]["beside_ms"], float(res["xt"]["exchanges"])],
+                            dtype=torch.float64)
+        xrows = [torch.zeros_like(xrow) for _ in range(world)]
+        dist.all_gather(xrows, xrow)
+        xts = [{"transfer_ms": float(r[0]), "beside_ms": float(r[1]), "exchanges": int(r[2])} for r in xrows]
         got = None
         if not args.no_check:
             width = plan["grid"][2] // world + 1
@@ -684,7 +692,7 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
                                                       "untimed full rounds (the same count on every rank), after one "
                                                       "full and one remainder round"),
                                         slab_plan={k: v for k, v in plan.items() if k != "grid"}),
-                      calibrate=on_gpu, emit=on_gpu)
+                      calibrate=on_gpu, emit=on_gpu, exchange=exchange_summary(xts, "rank"))
         return line, got, res
     return None, got, res
 
@@ -742,6 +750,7 @@ def main_slab_job(args):
     job.kernel_timing(True)
     job.run(extra)
     kt = job.kernel_time()
+    xt = job.exchange_time()
     job.kernel_timing(False)
     sweeps += extra
     sums = job.plane_sums() if not args.no_check else None
@@ -779,12 +788,33 @@ def main_slab_job(args):
                                                                     "remainder round"),
                              **({"rehearsal_check": check} if loop else {}),
                              **({"rank_of": args.rank_of, "global_grid": list(rank_plan["grid"])} if args.rank_of
-                                else {})))
+                                else {})),
+           exchange=exchange_summary([xt], "slab 0"))
+
+
+def exchange_summary(xts, who):
+    """The `exchange` object of a slab line: per rank (or slab 0), the mean
+    transfer time per timed round on its exchange stream and the fraction of
+    it that ran beside the same round's timed launches
+    (stencil_slab_exchange_time)."""
+    rows = []
+    for x in xts:
+        n = max(1, x["exchanges"])
+        rows.append({"transfer_ms_per_round": round(x["transfer_ms"] / n, 4),
+                     "beside_launch_frac": round(x["beside_ms"] / x["transfer_ms"], 3) if x["transfer_ms"] > 0 else None,
+                     "rounds": x["exchanges"]})
+    fracs = [r["beside_launch_frac"] for r in rows if r["beside_launch_frac"] is not None]
+    return {"basis": f"hipEvents on {who}'s exchange stream over the timed extra rounds: from the end of the face "
+                     "wait (or face launches) to the end of the RCCL send/recv; beside = the part that ran while the "
+                     "same round's timed launches ran",
+            "max_transfer_ms_per_round": max(r["transfer_ms_per_round"] for r in rows) if rows else None,
+            "min_beside_launch_frac": min(fracs) if fracs else None,
+            "per_rank" if len(rows) > 1 else "slab0": rows if len(rows) > 1 else rows[0]}
 
 
 def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_launch, sweeps_per_launch,
            kernel_launches, parallelism, rounds, launch_timing, workload_key, local, check, cpu, extra_config=None,
-           kernels_per_launch=1.0, calibrate=True, emit=True, cpu_full=False):
+           kernels_per_launch=1.0, calibrate=True, emit=True, cpu_full=False, exchange=None):
     """Print the one JSON line.  Roofline of the dominant kernel: one launch
     advances its cells by `sweeps_per_launch` fused sweeps; its compulsory HBM
     traffic is one read plus one write of those cells (2 * sizeof(T) per cell,
@@ -856,6 +886,8 @@ def report(args, pre, spec, kname, grid, n_gpus, elapsed, launch_ms, cells_per_l
     }
     if extra_config:
         out["config"].update(extra_config)
+    if exchange is not None:
+        out["exchange"] = exchange
     if n_gpus > 1:
         out["multi_gpu_check"] = check if check is not None else {"skipped": "--no-check"}
         out["multi_gpu_status"] = ("the rounds' code (csrc/slab_core.hpp) is bitwise-tested at world 2/3 on the CPU "

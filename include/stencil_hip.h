@@ -425,6 +425,15 @@ int stencil_slab_plane_sums(stencil_slab_job* job, double* sums);
 int stencil_slab_kernel_timing(stencil_slab_job* job, int32_t enable);
 int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* launches, int64_t* cells_per_launch,
                              int32_t* signalled);
+/* With kernel timing on, every timed round also records its exchange on slab
+ * 0's exchange stream: from the end of what precedes the transfers there (the
+ * face wait of a face-signalled round; a rolling round's face launches) to
+ * the end of the RCCL send/recv (or copies).  exchange_time synchronises and
+ * returns the summed transfer time, the part of it that ran while the same
+ * round's timed launch span ran (the overlap the round form is for; ~0 for
+ * serial rounds), and the exchanges counted.  Over xGMI this is the wire
+ * time of K planes per shared face plus RCCL's own latency. */
+int stencil_slab_exchange_time(stencil_slab_job* job, float* transfer_ms, float* beside_ms, int64_t* exchanges);
 /* The form of the job's full rounds (kernel_time's `signalled` is 1 for
  * face-signalled rounds, 0 otherwise). */
 enum {

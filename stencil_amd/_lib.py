@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "stencil_slab_upload", "stencil_slab_download", "stencil_slab_run", "stencil_slab_plane_sums",
     "stencil_slab_kernel_timing", "stencil_slab_kernel_time", "stencil_slab_unique_id", "stencil_slab_create_rank",
     "stencil_slab_create2", "stencil_slab_create_rank2", "stencil_slab_rolling_info", "stencil_slab_round_form",
-    "stencil_slab_set_timeout", "stencil_prepare2",
+    "stencil_slab_set_timeout", "stencil_prepare2", "stencil_slab_exchange_time",
 )
 
 
@@ -191,6 +191,7 @@ def signatures() -> dict:
                                              POINTER(c_int32)]),
         "stencil_slab_round_form": (c_int, [c_void_p, POINTER(c_int32)]),
         "stencil_slab_set_timeout": (c_int, [c_void_p, c_int64]),
+        "stencil_slab_exchange_time": (c_int, [c_void_p, POINTER(c_float), POINTER(c_float), POINTER(c_int64)]),
     }
 
 

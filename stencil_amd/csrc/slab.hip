@@ -546,6 +546,10 @@ int stencil_slab_kernel_time(stencil_slab_job* job, float* total_ms, int64_t* la
     return core::kernel_time<HipDev>(job, total_ms, launches, cells_per_launch, signalled);
 }
 
+int stencil_slab_exchange_time(stencil_slab_job* job, float* transfer_ms, float* beside_ms, int64_t* exchanges) {
+    return core::exchange_time<HipDev>(job, transfer_ms, beside_ms, exchanges);
+}
+
 int stencil_slab_plane_sums(stencil_slab_job* job, double* sums) {
     return core::plane_sums<HipDev>(job, sums);
 }

@@ -121,6 +121,11 @@ struct Job {
     std::vector<std::pair<typename Dev::Event, typename Dev::Event>> tev;
     int64_t timed_cells = 0;
     int64_t timed_launches = 0;  // kernel launches inside the timed spans
+    // with timing on, the exchange of each timed round on slab 0's X: from
+    // the end of what precedes the transfers there (a face wait) to the end
+    // of the transfers; xev[i] belongs to the round of tev[i]
+    std::vector<std::pair<typename Dev::Event, typename Dev::Event>> xev;
+    bool xopen = false;
     // bounded-time failure: every wait for the devices gives up after
     // timeout_ms (a peer that stopped posting leaves RCCL's receive spinning);
     // the job then aborts its communicators and every later call fails with
@@ -197,6 +202,28 @@ int time_end(Job<Dev>& j, size_t slab, typename Dev::Stream st, int64_t cells, i
     j.timed_launches += launches;
     return Dev::event_record(j.tev.back().second, st);
 }
+// the exchange span of the round whose launch span is open (slab 0 only;
+// fill / upload exchanges, outside any round, are not timed)
+template <class Dev>
+int xspan_begin(Job<Dev>& j, const Slab<Dev>& s) {
+    if (!j.timing || &s != &j.s[0] || j.xev.size() >= j.tev.size()) return STENCIL_OK;
+    typename Dev::Event a{}, b{};
+    SLAB_TRY(Dev::event_create(&a, true));
+    if (int rc = Dev::event_create(&b, true)) {
+        Dev::event_destroy(a);
+        return rc;
+    }
+    j.xev.emplace_back(a, b);
+    j.xopen = true;
+    return Dev::event_record(a, s.sx);
+}
+template <class Dev>
+int xspan_end(Job<Dev>& j, const Slab<Dev>& s) {
+    if (!j.xopen || &s != &j.s[0]) return STENCIL_OK;
+    j.xopen = false;
+    return Dev::event_record(j.xev.back().second, s.sx);
+}
+
 template <class Dev>
 void drop_timing(Job<Dev>& j) {
     for (auto& e : j.tev) {
@@ -204,6 +231,12 @@ void drop_timing(Job<Dev>& j) {
         Dev::event_destroy(e.second);
     }
     j.tev.clear();
+    for (auto& e : j.xev) {
+        Dev::event_destroy(e.first);
+        Dev::event_destroy(e.second);
+    }
+    j.xev.clear();
+    j.xopen = false;
     j.timed_cells = 0;
     j.timed_launches = 0;
 }
@@ -233,6 +266,7 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
         SLAB_TRY(Dev::event_record(s.ev_xin, s.sa));
         SLAB_TRY(Dev::stream_wait(s.sx, s.ev_xin));
         SLAB_TRY(pre(s));
+        SLAB_TRY(xspan_begin(j, s));
         if (j.tuning) SLAB_TRY(Dev::event_record(s.tx0, s.sx));
         // tests / rehearsals: the transfer's wire time between distinct GPUs (a no-op unless asked for)
         SLAB_TRY(Dev::wire_delay(s.sx, size_t(d) * plane_bytes(s)));
@@ -283,6 +317,7 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
         if (j.tuning) SLAB_TRY(Dev::event_record(s.tx1, s.sx));
+        SLAB_TRY(xspan_end(j, s));
         SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
     }
     for (int i = 0; i < n; ++i) {
@@ -556,6 +591,7 @@ int slab_round_rolling_overlap(Job<Dev>& j, int k) {
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
         SLAB_TRY(Dev::stream_wait(s.sx, s.ev_join));
+        SLAB_TRY(xspan_begin(j, s));
         SLAB_TRY(Dev::wire_delay(s.sx, size_t(d) * plane_bytes(s)));  // rehearsals: a distinct GPU's wire time
     }
     if (j.exchange == STENCIL_EXCHANGE_RCCL) {
@@ -597,6 +633,7 @@ int slab_round_rolling_overlap(Job<Dev>& j, int k) {
     }
     for (Slab<Dev>& s : j.s) {
         SLAB_TRY(Dev::set_device(s.device));
+        SLAB_TRY(xspan_end(j, s));
         SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
     }
     // 3. the pass, 4. the halos out of the staging
@@ -1260,6 +1297,35 @@ int kernel_time(JobT* job, float* total_ms, int64_t* launches, int64_t* cells_pe
     if (launches) *launches = int64_t(job->tev.size());
     if (cells_per_launch) *cells_per_launch = job->timed_cells;
     if (signalled) *signalled = job->signal ? 1 : 0;  // stencil_slab_round_form: the form
+    clear_error();
+    return STENCIL_OK;
+}
+
+// The exchanges of the timed rounds against their launch spans: the summed
+// transfer time on slab 0's X (from the end of its face wait, or of the face
+// launches it follows, to the end of the transfers) and the part of it that
+// ran while the same round's timed launch span was running (both on one
+// device clock).  Serial rounds: ~0 beside.
+template <class Dev, class JobT>
+int exchange_time(JobT* job, float* transfer_ms, float* beside_ms, int64_t* exchanges) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    SLAB_TRY(sync_bounded(*job));
+    SLAB_TRY(Dev::set_device(job->s[0].device));
+    double tsum = 0.0, bsum = 0.0;
+    int64_t n = 0;
+    const size_t m = std::min(job->tev.size(), job->xev.size() - (job->xopen ? 1 : 0));
+    for (size_t i = 0; i < m; ++i) {
+        float L = 0.f, a = 0.f, b = 0.f;
+        SLAB_TRY(Dev::event_elapsed(&L, job->tev[i].first, job->tev[i].second));
+        SLAB_TRY(Dev::event_elapsed(&a, job->tev[i].first, job->xev[i].first));
+        SLAB_TRY(Dev::event_elapsed(&b, job->tev[i].first, job->xev[i].second));
+        tsum += std::max(0.f, b - a);
+        bsum += std::max(0.f, std::min(L, b) - std::max(0.f, a));
+        ++n;
+    }
+    if (transfer_ms) *transfer_ms = float(tsum);
+    if (beside_ms) *beside_ms = float(bsum);
+    if (exchanges) *exchanges = n;
     clear_error();
     return STENCIL_OK;
 }

@@ -461,6 +461,15 @@ class SlabJob:
         return {"total_ms": float(ms.value), "launches": int(n.value), "cells_per_launch": int(cells.value),
                 "signalled": int(sig.value) == 1, "rolling": form == 2, "serial": form == 3, "form": form}
 
+    def exchange_time(self) -> dict:
+        """The timed rounds' exchanges (kernel timing on): summed transfer time
+        on slab 0's exchange stream, the part of it beside the same round's
+        timed launches, and the count (stencil_slab_exchange_time)."""
+        t, b, n = ctypes.c_float(0.0), ctypes.c_float(0.0), ctypes.c_int64(0)
+        _lib.check(self.lib.stencil_slab_exchange_time(self.job, ctypes.byref(t), ctypes.byref(b), ctypes.byref(n)),
+                   "stencil_slab_exchange_time", lib=self.lib)
+        return {"transfer_ms": float(t.value), "beside_ms": float(b.value), "exchanges": int(n.value)}
+
     def round_form(self) -> int:
         """0 boundary + interior launches, 1 face-signalled, 2 rolling passes, 3 serial, 4 staged."""
         f = ctypes.c_int32(-1)

@@ -627,6 +627,9 @@ int fake_slab_kernel_timing(fake_slab_job* job, int32_t enable) { return core::k
 int fake_slab_kernel_time(fake_slab_job* job, float* ms, int64_t* n, int64_t* cells, int32_t* sig) {
     return core::kernel_time<FakeDev>(job, ms, n, cells, sig);
 }
+int fake_slab_exchange_time(fake_slab_job* job, float* transfer_ms, float* beside_ms, int64_t* n) {
+    return core::exchange_time<FakeDev>(job, transfer_ms, beside_ms, n);
+}
 int fake_slab_plane_sums(fake_slab_job* job, double* sums) { return core::plane_sums<FakeDev>(job, sums); }
 // the fake's layout arithmetic, compared with the product's stencil_layout_init
 int fake_slab_layout_init(const stencil_problem* p, stencil_layout* out) { return FakeDev::layout_init(p, out); }

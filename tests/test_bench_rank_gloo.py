@@ -80,6 +80,11 @@ def test_bench_rank_job_world_gloo(world, config, extra):
         cfg = line["config"]
         assert cfg["settle_launches"] >= 1 and cfg["settle_ms"] >= 0 and "settle" in cfg
         assert "effective_GBps_whole_job" in cfg and "achieved_hbm_GBps_whole_job" not in cfg
+        # every rank's exchange of the timed rounds is on the line: one per timed round
+        ex = line["exchange"]
+        assert len(ex["per_rank"]) == world, ex
+        assert all(r["rounds"] == line["roofline"]["launches"] for r in ex["per_rank"]), ex
+        assert ex["max_transfer_ms_per_round"] >= 0
     # the same sweeps on ONE slab (no exchange), the fake device's plane sums
     fake = fb.load()
     fake.set_k(0)

@@ -581,3 +581,30 @@ def test_missing_rank_fails_communicator_creation_in_time(gpu):
     assert 1.5 < res["took"] < 10.0, res
     assert "not every rank joined" in res["msg"], res
     assert time.monotonic() - t0 < 60.0
+
+
+@pytest.mark.parametrize("form", ["signalled", "serial"])
+def test_exchange_time_beside_the_launch(gpu, monkeypatch, form):
+    """stencil_slab_exchange_time on the HIP path: an interior-rank rehearsal
+    (one periodic slab, RCCL to itself) records one exchange per timed round;
+    face-signalled rounds run most of the transfer beside their launch,
+    serial rounds none of it."""
+    monkeypatch.setenv("STENCIL_SLAB_SERIAL", "1" if form == "serial" else "0")
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 512, 512, 128, [gpu], exchange="rccl", periodic=True)
+    try:
+        assert job.round_form() == (1 if form == "signalled" else 3)
+        job.fill_initial("reference")
+        job.run(8)
+        job.kernel_timing(True)
+        job.run(24)
+        kt, xt = job.kernel_time(), job.exchange_time()
+        assert kt["launches"] == 6 and xt["exchanges"] == 6, (kt, xt)
+        assert xt["transfer_ms"] > 0 and 0 <= xt["beside_ms"] <= xt["transfer_ms"] + 1e-3, xt
+        frac = xt["beside_ms"] / xt["transfer_ms"]
+        if form == "signalled":
+            assert frac > 0.5, xt
+        else:
+            assert frac < 0.05, xt
+    finally:
+        job.close()

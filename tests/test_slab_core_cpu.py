@@ -354,6 +354,40 @@ def test_missing_rank_fails_creation_in_bounded_time(fake, monkeypatch, present)
         assert 0.5 < res[r][1] < 5.0, res
 
 
+@pytest.mark.parametrize("case", ["signalled", "boundary", "staged", "rolling", "serial"])
+def test_exchange_time_pairs_every_timed_round(fake, monkeypatch, case):
+    """stencil_slab_exchange_time: with kernel timing on, each timed round
+    (full or remainder) records one exchange span on slab 0's exchange
+    stream, paired with its launch span; fill / upload exchanges are not
+    counted; beside <= transfer."""
+    k = 4
+    fake.set_k(k)
+    fake.set_signal(case in ("signalled", "staged"))
+    if case == "staged":  # the fake's stand-in for a grid of several rounds of workgroups
+        monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
+    if case == "serial":
+        monkeypatch.setenv("STENCIL_SLAB_SERIAL", "1")
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 10, 6, 40, [0, 1], exchange="rccl", rolling=case == "rolling", margin=k + 2, lib=fake)
+    try:
+        assert job.round_form() == {"signalled": 1, "boundary": 0, "staged": 4, "rolling": 2, "serial": 3}[case]
+        job.fill_initial("reference")
+        job.run(k)
+        job.kernel_timing(True)
+        job.run(3 * k + 1)  # three full rounds and a remainder round
+        kt = job.kernel_time()
+        xt = job.exchange_time()
+        assert kt["launches"] == 4 and xt["exchanges"] == 4, (kt, xt)
+        assert 0.0 <= xt["beside_ms"] <= xt["transfer_ms"] + 1e-3, xt
+        job.fill_initial("reference")  # fill's exchanges are outside any round
+        assert job.exchange_time()["exchanges"] == 4
+        job.kernel_timing(False)
+        assert job.exchange_time()["exchanges"] == 0
+    finally:
+        job.close()
+        fake.set_signal(True)
+
+
 def test_upload_checks_the_rolling_ghost_ring(fake):
     """ROLLING slabs need the same x/y ghost ring in every plane:
     upload refuses a host grid whose ring varies with z, and takes it for a
