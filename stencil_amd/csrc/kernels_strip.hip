@@ -52,6 +52,9 @@
 #ifndef TK_FAST_PATH
 #define TK_FAST_PATH 1
 #endif
+#ifndef TK_PACK2
+#define TK_PACK2 1
+#endif
 
 namespace stencil {
 namespace {
@@ -418,6 +421,8 @@ __global__ void __launch_bounds__(64 * NW)
     auto stepb = [&](auto S_, int p, auto FAST_) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % LCM
         constexpr bool FAST = decltype(FAST_)::value;  // no ghost-cell selects this step
+        // fp32 two cells per lane: packed math (-DTK_PACK2=0 builds keep the scalar loop)
+        constexpr bool kPack2 = TK_PACK2 && sizeof(T) == 4 && V == 2;
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
         constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
         if constexpr (TIER) {
@@ -483,6 +488,24 @@ __global__ void __launch_bounds__(64 * NW)
                 const T wl = sdpp<kSShr1>(c[V - 1]);
                 const T er = sdpp<kSShl1>(c[0]);
                 VT o;
+                if constexpr (kPack2) {
+                    // fp32 pairs: the same sums as the loop below, the x
+                    // pair scalar (its lane shifts fold into v_add_f32_dpp),
+                    // the rest in packed math (v_pk_add_f32 / v_pk_fma_f32:
+                    // both cells of the lane per instruction, each
+                    // IEEE-rounded as the scalar op)
+                    VT sum = VT{wl + c[1], c[0] + er};
+                    sum += up;
+                    sum += dn;
+                    sum += REV ? zp : zm;
+                    sum += REV ? zm : zp;
+                    o = DIAG == 2 ? c : __builtin_elementwise_fma(sum, VT{avg, avg}, VT{});
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
+                        if (PROD && s == K && !FAST) o[j] = (yin[k] && xin[j]) ? o[j] : c[j];
+                    }
+                } else {
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
                     T sum = (j == 0 ? wl : c[j - 1]) + (j == V - 1 ? er : c[j + 1]);
@@ -496,6 +519,7 @@ __global__ void __launch_bounds__(64 * NW)
                     if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
                     // TIER producer: t_K keeps the ghost cells too (they go to the slots)
                     if (PROD && s == K && !FAST) o[j] = (yin[k] && xin[j]) ? o[j] : c[j];
+                }
                 }
                 // t_{s-1}(p-s+1) takes the slot of t_{s-1}(p-s-1), consumed just now
                 if constexpr (s >= 2) hset(s - 1, (S - s + 5) & 1, k, prev);
