@@ -118,6 +118,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
+    ap.add_argument("--placements", type=int, default=6,
+                    help="single-GPU two-grid configs: grid placements tried before the run (the fastest kept; "
+                         "1 = the first allocation)")
     ap.add_argument("--no-signal", action="store_true",
                     help="multi-GPU rounds as separate boundary/interior launches (no face counters; "
                          "STENCIL_SLAB_SIGNAL=0)")
@@ -462,6 +465,9 @@ def main_single(args):
         key = "C3_rolling_4096" if args.config == "C3" else f"{args.config}_rolling"
     else:
         eng = JacobiEngine(spec, gnx, gny, gnz, device=0)
+        # where the grids' pages land moves the launch by up to 8 %: the
+        # engine picks the fastest of a few placements (untimed; §9.1j)
+        placement = eng.place(trials=args.placements) if args.placements > 1 else None
         eng.reset(args.init, INIT_SEED)
         kernel_id = eng.plan(12)[1]
         kname = {1: "direct", 2: "zmarch", 3: "temporal2", 4: "temporalk"}[kernel_id]
@@ -483,6 +489,10 @@ def main_single(args):
         extra, kernels_per_launch = settle_config(settle["launches"], settle["device_ms"],
                                                   "stencil_prepare2: the schedule trial + ~25 ms of the job's own "
                                                   "launch (a -> b, grid a unchanged)"), 1.0
+        if placement is not None:
+            extra["placement"] = dict(placement, basis="JacobiEngine.place: candidate grid pairs allocated while "
+                                                       "the earlier ones are held, one fused launch timed on each "
+                                                       "(untimed region), the fastest kept")
         parallelism = "1 GPU, one process, the whole grid (no decomposition)"
         timing = "hipEvents of stencil_iterate over the timed region"
         key = f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz}"

@@ -636,6 +636,10 @@ def test_c2_whole_benched_job_against_oracle(gpu):
     e = engine(gpu, 3, "fp64", "star", 1, "naive", "auto", n, n, n)
     assert e.fuse_steps == 4
     assert e.plan(it) == (250, _lib.KERNEL_TEMPORALK)
+    # bench.py first picks the fastest of a few grid placements
+    placed = e.place(trials=3)
+    assert placed["candidates"] == 3 and 0 <= placed["chosen"] < 3
+    assert placed["ms_per_launch"][placed["chosen"]] == min(placed["ms_per_launch"])
     e.reset()
     e.prepare()  # bench.py settles the schedule first; grid a is unchanged
     fin, _ = e.iterate(it)
