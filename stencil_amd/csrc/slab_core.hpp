@@ -42,6 +42,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -91,6 +92,10 @@ struct Slab {
     // the timing events of the tuning rounds (B on its stream, the exchange)
     int64_t face_span = 0;
     typename Dev::Event tb0{}, tb1{}, tx0{}, tx1{};
+    // the grid placement chosen at creation (place_grids): candidates tried
+    // and the chosen pair's ms per K-step launch
+    int placements = 1;
+    float placement_ms = 0.f;
 };
 
 template <class Dev>
@@ -825,6 +830,78 @@ int rolling_margin(const Job<Dev>& j, const stencil_layout& l, int64_t want, int
     return STENCIL_OK;
 }
 
+// Where a slab's two grids live: the same launch runs 4-8 %
+// apart depending on which physical pages its grids occupy.  Up to
+// Dev::placement_trials() candidate pairs (each allocated while the earlier
+// ones are held, within a quarter of the free memory), one K-step launch of
+// the whole slab timed on each in two interleaved passes, the fastest pair
+// kept and the rest freed.  Values do not matter (the grids are filled
+// before the job starts); every rank chooses alone, no collective.
+template <class Dev>
+int place_grids(const Job<Dev>& j, Slab<Dev>& s) {
+    const int trials = Dev::placement_trials();
+    if (trials <= 1 || !s.a || !s.b) return STENCIL_OK;
+    const int64_t bytes = s.l.bytes + 256;
+    int64_t free_b = 0;
+    SLAB_TRY(Dev::free_bytes(&free_b));
+    const int64_t extra = std::min<int64_t>(trials - 1, free_b / 4 / std::max<int64_t>(1, 2 * bytes));
+    if (extra <= 0) return STENCIL_OK;
+    std::vector<std::pair<void*, void*>> cand{{s.a, s.b}};
+    typename Dev::Event e0{}, e1{};
+    int rc = Dev::event_create(&e0, true);
+    if (rc == STENCIL_OK) rc = Dev::event_create(&e1, true);
+    for (int64_t i = 0; i < extra && rc == STENCIL_OK; ++i) {
+        void* a = nullptr;
+        void* b = nullptr;
+        if (Dev::alloc(bytes, &a) != STENCIL_OK) break;  // no room: fewer candidates
+        if (Dev::alloc(bytes, &b) != STENCIL_OK) {
+            Dev::free(a);
+            break;
+        }
+        cand.emplace_back(a, b);
+    }
+    clear_error();
+    std::vector<float> best(cand.size(), 1e30f);
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(j.timeout_ms);
+    for (auto& c : cand)
+        for (void* g : {c.first, c.second})
+            if (rc == STENCIL_OK) rc = Dev::fill_initial(&s.l, g, STENCIL_INIT_REFERENCE, 0, s.sa);
+    for (int w = 0; w < 8 && rc == STENCIL_OK; ++w)  // clock up before the first candidate is timed
+        rc = Dev::sweepk(&s.l, cand[0].first, cand[0].second, 0, s.n, j.k, s.sa);
+    for (int pass = 0; pass < 2 && rc == STENCIL_OK; ++pass)
+        for (size_t i = 0; i < cand.size() && rc == STENCIL_OK; ++i)
+            for (int t = 0; t < 3 && rc == STENCIL_OK; ++t) {  // one untimed, two timed launches
+                if (t) rc = Dev::event_record(e0, s.sa);
+                if (rc == STENCIL_OK) rc = Dev::sweepk(&s.l, cand[i].first, cand[i].second, 0, s.n, j.k, s.sa);
+                if (t && rc == STENCIL_OK) rc = Dev::event_record(e1, s.sa);
+                if (t && rc == STENCIL_OK) rc = Dev::sync_until(s.sa, typename Dev::Comm{}, deadline);
+                float ms = 0.f;
+                if (t && rc == STENCIL_OK) rc = Dev::event_elapsed(&ms, e0, e1);
+                if (t && rc == STENCIL_OK) best[i] = std::min(best[i], ms);
+            }
+    size_t pick = 0;
+    for (size_t i = 1; i < cand.size(); ++i)
+        if (best[i] < best[pick]) pick = i;
+    if (rc != STENCIL_OK) pick = 0;  // keep the first pair; the error is returned
+    if (e0) Dev::event_destroy(e0);
+    if (e1) Dev::event_destroy(e1);
+    for (size_t i = 0; i < cand.size(); ++i)
+        if (i != pick) {
+            Dev::free(cand[i].first);
+            Dev::free(cand[i].second);
+        }
+    if (Dev::placement_verbose()) {
+        std::fprintf(stderr, "[slab %d] placement: %zu candidates, ms per launch:", s.index, cand.size());
+        for (float v : best) std::fprintf(stderr, " %.4f", double(v));
+        std::fprintf(stderr, "; chose %zu\n", pick);
+    }
+    s.a = cand[pick].first;
+    s.b = cand[pick].second;
+    s.placement_ms = rc == STENCIL_OK ? best[pick] : 0.f;
+    s.placements = int(cand.size());
+    return rc;
+}
+
 // The slabs this process owns: global slab indices `idx` (of `total`) on
 // `devs`; the z split is the same in every process (planes total / N, the first
 // nz % N slabs one more), so each rank can build its own share alone.
@@ -940,6 +1017,7 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
         if (rc) break;
         if ((rc = Dev::alloc_counters(&s.counters)) || (rc = Dev::alloc_flag(&s.tflag))) break;
         if (j->signal && (rc = Dev::face_signal_create(&s.fsig))) break;
+        if (!rolling && (rc = place_grids(*j, s))) break;
     }
     if (rc != STENCIL_OK) {
         release<Dev>(j);

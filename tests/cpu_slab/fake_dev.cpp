@@ -243,6 +243,12 @@ struct FakeDev {
         const char* v = std::getenv("FAKE_SLAB_CONFINE");
         return v && std::atoi(v) != 0;
     }
+    // FAKE_SLAB_PLACE=n: the placement search's allocation and choice logic (timings are the host's)
+    static int placement_trials() {
+        const char* v = std::getenv("FAKE_SLAB_PLACE");
+        return v && std::atoi(v) > 1 ? std::atoi(v) : 1;
+    }
+    static bool placement_verbose() { return false; }
     static bool staged_rounds() {
         const char* v = std::getenv("STENCIL_SLAB_STAGED");
         return !(v && *v && std::atoi(v) == 0);

@@ -322,6 +322,24 @@ def test_silent_peer_fails_every_rank_in_bounded_time(fake, monkeypatch, nranks,
         assert again[0] == _lib.ETIMEOUT and "failed earlier" in again[1], again
 
 
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+def test_grid_placement_search_keeps_results(fake, monkeypatch, nslabs):
+    """place_grids with 3 candidate pairs per slab
+    (FAKE_SLAB_PLACE=3): the chosen pair runs the job, the others are freed,
+    and the result is bitwise the oracle's one grid."""
+    monkeypatch.setenv("FAKE_SLAB_PLACE", "3")
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 11, 6, 9 * nslabs + 1
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange="rccl", lib=fake)
+    try:
+        job.fill_initial("random", 4)
+        job.run(10)
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, 10, seed=4))
+    finally:
+        job.close()
+
+
 @pytest.mark.parametrize("present", [1, 2])
 def test_missing_rank_fails_creation_in_bounded_time(fake, monkeypatch, present):
     """Communicator creation is a collective: with a rank that never calls
