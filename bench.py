@@ -467,6 +467,8 @@ def main_single(args):
         eng = JacobiEngine(spec, gnx, gny, gnz, device=0)
         # where the grids' pages land moves the launch by up to 8 %: the
         # engine picks the fastest of a few placements (untimed; §9.1j)
+        # (candidates within a quarter of the free memory: C2 gets 6; the 70 GB grids of NS / C5 none --
+        # measured with one extra pair each, their two placements ran within 0.6 %, r05ap)
         placement = eng.place(trials=args.placements) if args.placements > 1 else None
         eng.reset(args.init, INIT_SEED)
         kernel_id = eng.plan(12)[1]

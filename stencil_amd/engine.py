@@ -121,7 +121,12 @@ class JacobiEngine:
             return {"candidates": 1, "ms_per_launch": [], "chosen": 0, "sweeps_per_launch": self.fuse_steps}
         cands = [(self.a, self.b)]
         for _ in range(n - 1):
-            cands.append((torch.empty_like(self.a), torch.empty_like(self.b)))
+            try:
+                cands.append((torch.empty_like(self.a), torch.empty_like(self.b)))
+            except torch.OutOfMemoryError:  # fewer candidates
+                break
+        if len(cands) == 1:
+            return {"candidates": 1, "ms_per_launch": [], "chosen": 0, "sweeps_per_launch": self.fuse_steps}
         k = self.fuse_steps if self.fused else 1
         fin, ms = ctypes.c_int(0), ctypes.c_float(0.0)
         stream = _stream_handle(None)
@@ -144,7 +149,8 @@ class JacobiEngine:
                 best[i] = min(best[i], run(a, b, True), run(a, b, True))
         pick = min(range(len(cands)), key=lambda i: best[i])
         self.a, self.b = cands[pick]
-        del cands
+        a = b = None  # drop every reference to the other candidates before returning their memory
+        cands.clear()
         torch.cuda.empty_cache()
         return {"candidates": len(best), "ms_per_launch": [round(v, 5) for v in best], "chosen": pick,
                 "sweeps_per_launch": k}
