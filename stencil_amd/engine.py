@@ -99,7 +99,7 @@ class JacobiEngine:
         self.fill_initial(self.a, kind, seed)
         self.fill_initial(self.b, kind, seed)
 
-    def place(self, trials: int = 6, max_bytes: int | None = None, passes: int = 2) -> dict:
+    def place(self, trials: int = 6, max_bytes: int | None = None, passes: int = 2, sweeps: int | None = None) -> dict:
         """Choose where the two grids live.  The same launch
         runs up to 8 % apart depending on which physical pages its grids land
         on (512^3 fp64: 1184-1278 Gcell/s over 18 placements in one process;
@@ -110,7 +110,8 @@ class JacobiEngine:
         per pass), keep the fastest pair and free the rest.  The grids'
         contents are undefined afterwards: call reset().  Candidates are
         limited to `max_bytes` (default a quarter of the free memory).
-        Returns the per-candidate ms per launch and the choice."""
+        `sweeps`: the sweeps each timed call runs (default one fused launch).
+        Returns the per-candidate ms per call and the choice."""
         if not hasattr(self, "a"):
             raise ValueError("place() needs the engine's grids (allocate=True)")
         grid_bytes = self.a.numel() * self.a.element_size()
@@ -127,7 +128,7 @@ class JacobiEngine:
                 break
         if len(cands) == 1:
             return {"candidates": 1, "ms_per_launch": [], "chosen": 0, "sweeps_per_launch": self.fuse_steps}
-        k = self.fuse_steps if self.fused else 1
+        k = int(sweeps) if sweeps else (self.fuse_steps if self.fused else 1)
         fin, ms = ctypes.c_int(0), ctypes.c_float(0.0)
         stream = _stream_handle(None)
 
