@@ -118,7 +118,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=512, help="per-GPU cube edge (config 2: 512)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "direct", "zmarch", "temporal2"])
-    ap.add_argument("--placements", type=int, default=6,
+    ap.add_argument("--placements", type=int, default=16,
                     help="single-GPU two-grid configs: grid placements tried before the run (the fastest kept; "
                          "1 = the first allocation)")
     ap.add_argument("--no-signal", action="store_true",
@@ -467,7 +467,7 @@ def main_single(args):
         eng = JacobiEngine(spec, gnx, gny, gnz, device=0)
         # where the grids' pages land moves the launch by up to 8 %: the
         # engine picks the fastest of a few placements (untimed; §9.1j)
-        # (candidates within a quarter of the free memory: C2 gets 6; the 70 GB grids of NS / C5 none --
+        # (candidates within a quarter of the free memory: C2 gets 16; the 70 GB grids of NS / C5 none --
         # measured with one extra pair each, their two placements ran within 0.6 %, r05ap)
         placement = eng.place(trials=args.placements) if args.placements > 1 else None
         eng.reset(args.init, INIT_SEED)
