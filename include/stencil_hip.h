@@ -71,7 +71,7 @@ int stencil_last_error(void);
  * its exchange confined to c CUs of every XCD and its launches off them;
  * 0 = never confined) and STENCIL_SLAB_XCU_EXCL=0 (the launches may use the
  * exchange's CUs too),
- * STENCIL_SLAB_PLACEMENTS=n (default 6: a two-grid slab tries n placements
+ * STENCIL_SLAB_PLACEMENTS=n (default 16: a two-grid slab tries n placements
  * of its grids at creation and keeps the fastest -- the same launch runs 4-8 %
  * apart depending on the grids' physical pages; 1 = the first allocation),
  * STENCIL_SLAB_TIMEOUT_MS (a slab job's deadline for any device wait,

@@ -158,8 +158,8 @@ struct HipDev {
     // exchange confined) instead of staged ones
     static bool staged_rounds() { return api_knob("STENCIL_SLAB_STAGED", 1) != 0; }
     // STENCIL_SLAB_PLACEMENTS=n: grid placements a two-grid slab tries at
-    // creation (default 6; 1 = the first allocation)
-    static int placement_trials() { return std::max(1, api_knob("STENCIL_SLAB_PLACEMENTS", 6)); }
+    // creation (default 16; 1 = the first allocation)
+    static int placement_trials() { return std::max(1, api_knob("STENCIL_SLAB_PLACEMENTS", 16)); }
     static bool placement_verbose() { return knob("STENCIL_SLAB_PLACE_VERBOSE", 0) != 0; }
     // STENCIL_SLAB_ROLLING_OVERLAP=0: rolling rounds exchange after the pass
     // (slab_round_rolling) instead of beside it (slab_round_rolling_overlap)

@@ -157,7 +157,7 @@ for step in "$@"; do
               wire*) envs+=(STENCIL_SLAB_WIRE_GBPS=${v#wire}) ;;   # emulated xGMI wire time (debug library)
               nox) envs+=(STENCIL_SLAB_XCU=0) ;; noexcl) envs+=(STENCIL_SLAB_XCU_EXCL=0) ;;
               nostage) envs+=(STENCIL_SLAB_STAGED=0) ;; spare*) envs+=(STENCIL_TK_SIG_SPARE=${v#spare}) ;;
-              noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
+              noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; place*) envs+=(STENCIL_SLAB_PLACEMENTS=${v#place}) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
               sig*) envs+=(STENCIL_TK_SIG_CHUNKS=${v#sig}) ;; bsig*) envs+=(STENCIL_BOXK_SIG_CHUNKS=${v#bsig}) ;;
               xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
               xcu*) envs+=(STENCIL_SLAB_XCU=${v#xcu}) ;;
@@ -168,6 +168,7 @@ for step in "$@"; do
           [ "$nr" != 0 ] && a="$a --rank-of $nr"
           a="$a --allow-debug-library"
           name="xr_${c}_${nr}_${ex}_${var}${tr:+_$tr}"
+          k2=1; while [ -e "$O/$name.json" ]; do k2=$((k2 + 1)); name="xr_${c}_${nr}_${ex}_${var}${tr:+_$tr}_$k2"; done
           if [ "$tr" = trace ]; then
             (cd /tmp && env "${envs[@]}" TMPDIR=/tmp timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv \
                -d "$O/$name" -o run -- python3 "$R/bench.py" --config "$c" --exchange "$ex" $a --no-cpu-baseline \
