@@ -778,11 +778,16 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         return STENCIL_OK;
     }
     // XCD-patch work order (STENCIL_TK_XCD = patch width, the box kernel's
-    // map): default 16 tiles wide for fp32 grids of more than two rounds of
-    // tiles -- 4096^2 x 256 fp32 K = 5 reads 32.1 -> 21.6 GB per launch
-    // (1.87x -> 1.25x compulsory) and runs 3 % faster, C3 2612 -> 2722
-    // Gcell/s; fp64 shapes within 0.5 % either way, so off
-    const int xcd_dflt = sizeof(T) == 4 && tiles > 2 * int64_t(slots) ? 16 : 0;
+    // map) for grids of more than two rounds of tiles: fp32 16 tiles wide --
+    // 4096^2 x 256 fp32 K = 5 reads 32.1 -> 21.6 GB per launch (1.87x ->
+    // 1.25x compulsory) and runs 3 % faster, C3 2612 -> 2722 Gcell/s; fp64 8
+    // wide on launches of a whole grid -- reads 1.76x -> 1.19x at 2048^2 x
+    // 512, NS 2048^3 1317 -> 1373 Gcell/s over three alternating sustained
+    // runs -- but not on slab launches (halo planes: the staged rounds ran
+    // 3.5 % slower, NS4096 rank of 4 1292 vs 1340) nor on z-range launches
+    // (rolling C4: 1262 vs 1351)
+    const bool whole = !halo && begin == 0 && end == g.nz;
+    const int xcd_dflt = tiles > 2 * int64_t(slots) ? (sizeof(T) == 4 ? 16 : (whole ? 8 : 0)) : 0;
     const int xcd_pw = !SIG && zc > 0 ? senv_int("STENCIL_TK_XCD", xcd_dflt) : 0;
     auto launch = [&](bool packed) {
         const int64_t n = packed ? nb : (xcd_pw > 0 ? (nb_equal + 7) / 8 * 8 : nb_equal);

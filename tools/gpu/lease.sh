@@ -157,7 +157,7 @@ for step in "$@"; do
               wire*) envs+=(STENCIL_SLAB_WIRE_GBPS=${v#wire}) ;;   # emulated xGMI wire time (debug library)
               nox) envs+=(STENCIL_SLAB_XCU=0) ;; noexcl) envs+=(STENCIL_SLAB_XCU_EXCL=0) ;;
               nostage) envs+=(STENCIL_SLAB_STAGED=0) ;; spare*) envs+=(STENCIL_TK_SIG_SPARE=${v#spare}) ;;
-              noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; place*) envs+=(STENCIL_SLAB_PLACEMENTS=${v#place}) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
+              tkxcd*) envs+=(STENCIL_TK_XCD=${v#tkxcd}) ;; noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; place*) envs+=(STENCIL_SLAB_PLACEMENTS=${v#place}) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
               sig*) envs+=(STENCIL_TK_SIG_CHUNKS=${v#sig}) ;; bsig*) envs+=(STENCIL_BOXK_SIG_CHUNKS=${v#bsig}) ;;
               xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
               xcu*) envs+=(STENCIL_SLAB_XCU=${v#xcu}) ;;
@@ -195,8 +195,10 @@ for step in "$@"; do
     envbench:*) # envbench:<NAME=V[,NAME=V]>:<cfg> -- bench.py --config cfg with those variables (debug library allowed)
           IFS=':' read -r ev c <<< "${step#envbench:}"
           case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+          f="$O/envbench_${c}_${ev//[=,]/_}.json"; k2=1
+          while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/envbench_${c}_${ev//[=,]/_}_$k2.json"; done
           env ${ev//,/ } timeout -k 10 400 python3 bench.py --config "$c" $a --no-cpu-baseline --allow-debug-library \
-            > "$O/envbench_${c}_${ev//[=,]/_}.json" 2>> "$O/bench.err" ;;
+            > "$f" 2>> "$O/bench.err" ;;
     xcdpmc:*) # xcdpmc:<dtype>:nx:ny:nz:steps:w -- FETCH_SIZE / WRITE_SIZE passes of that variant's launches
           IFS=':' read -r dt nx ny nz st w <<< "${step#xcdpmc:}"
           for ctr in FETCH_SIZE WRITE_SIZE; do
