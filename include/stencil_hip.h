@@ -78,7 +78,10 @@ int stencil_last_error(void);
  * default 60000: stencil_slab_set_timeout), STENCIL_SLAB_ROLLING_OVERLAP=0
  * (rolling slab rounds exchange after the pass instead of beside it),
  * STENCIL_SLAB_STAGED=0 (slabs whose launch takes several rounds of
- * workgroups run face-signalled rounds instead of staged ones). */
+ * workgroups run face-signalled rounds instead of staged ones),
+ * STENCIL_SLAB_GATE=0 (face-signalled rounds wait for the exchange stream's
+ * event before each launch instead of gating the launch's halo-reading
+ * workgroups on the exchange-completion word: stencil_slab_round_info). */
 int stencil_debug_knobs(void);
 
 /* --------------------------------------------- 1. reference-compatible ABI */
@@ -246,6 +249,21 @@ int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, in
                           void* stream);
 int stencil_wait_counters(const uint32_t* counters, uint32_t target_lo, uint32_t target_hi, uint32_t* timeout_flag,
                           void* stream);
+/* The halo-gated form (the 7-point star only; the box: STENCIL_EUNSUPPORTED):
+ * as stencil_sweepk_signal, and the workgroups whose z range reaches a halo
+ * plane (z < 0 with STENCIL_HALO_LO, z >= nz with STENCIL_HALO_HI) first wait
+ * until counters[3] >= gate_need (uint32, wrap-safe), until *release_flag != 0
+ * (host-coherent, as stencil_wait_counters' timeout flag; may be NULL), or
+ * 10 s (then they set *release_flag and go on with stale halos: the caller
+ * must treat the launch as failed).  A slab round then queues its launch right behind the previous
+ * round's launch, with no event wait for the exchange that fills its halos
+ * (DESIGN.md §7): the halo planes are the only bytes that exchange writes.
+ * stencil_exchange_done queues on `stream` (behind the exchange's transfers)
+ * one lane storing counters[3] = value. */
+int stencil_sweepk_signal_gated(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                                int32_t steps, uint32_t* counters, uint64_t* face_signal, uint32_t gate_need,
+                                uint32_t* release_flag, int32_t* signals_per_face, void* stream);
+int stencil_exchange_done(uint32_t* counters, uint32_t value, void* stream);
 /* face signals: 8 bytes of HIP signal memory (hipExtMallocWithFlags,
  * hipMallocSignalMemory) holding a uint64 count */
 int stencil_face_signal_create(uint64_t** face_signal);
@@ -447,6 +465,12 @@ enum {
     STENCIL_SLAB_FORM_STAGED = 4             /* the face quarters, then the middle beside the exchange */
 };
 int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form);
+/* How the job's full rounds run beyond their form (each output may be NULL):
+ * *gated = 1 when face-signalled launches gate their halo-reading workgroups
+ * on the exchange-completion word instead of waiting for the exchange stream
+ * (stencil_sweepk_signal_gated; STENCIL_SLAB_GATE=0: never), *confined = 1
+ * when the exchange runs on a few CUs of its own (STENCIL_SLAB_XCU). */
+int stencil_slab_round_info(const stencil_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined);
 /* Bounded-time failure.  Every wait of the job for its devices (the end of
  * run(), fill, upload, download, plane sums, and -- while run() issues
  * rounds -- the exchange of the round kInflight = 8 rounds back) gives up

@@ -285,6 +285,14 @@ __global__ void __launch_bounds__(64) wait_counters_kernel(const uint32_t* __res
     }
 }
 
+// The exchange-completion word of a slab (stencil_exchange_done): one lane's
+// relaxed agent-scope vector store, queued behind the exchange's transfers on
+// their stream (kernel boundaries order it after them); the gated launches
+// poll it (kernels_strip.hip gate_wait).
+__global__ void __launch_bounds__(64) exchange_done_kernel(uint32_t* __restrict__ word, uint32_t value) {
+    if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Streaming copy used to calibrate attainable HBM bandwidth: 4 independent
 // 16-B loads in flight per lane, one pass, no grid-stride loop.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -348,12 +356,15 @@ constexpr int64_t kPitchPeriod = 32768;  // bytes (stencil_layout_init's pitch r
 
 // The row-pitch rule (round 5): pitches of 32 KiB or more
 // whose residue r modulo 32 KiB lies in [-512, +256] B run the K-step kernels
-// 3-30 % slower; such a row is padded to residue 384 (r in [0, 256]) or by
-// 128 B (r in [-512, -128]).  Returns the bytes to add.
+// 3-30 % slower; such a row is padded to residue 384 (r in [-256, 256]) or by
+// 128 B (r in [-512, -257]: -512 measured fast at +128).  Residues -256 and
+// -128 go to 384 too: 128 B more would land them on -128 / 0, inside the slow
+// window.  Returns the bytes to add.
 int64_t pitch_pad_bytes(int64_t pitch) {
     if (pitch < kPitchPeriod - 512) return 0;
     const int64_t r = pitch % kPitchPeriod;
     if (pitch >= kPitchPeriod && r <= 256) return 384 - r;
+    if (r >= kPitchPeriod - 256) return kPitchPeriod - r + 384;
     if (r >= kPitchPeriod - 512) return 128;
     return 0;
 }
@@ -604,6 +615,38 @@ int stencil_sweepk_signal(const stencil_layout* l, const void* in, void* out, in
         clear_error();
     }
     return rc;
+}
+
+int stencil_sweepk_signal_gated(const stencil_layout* l, const void* in, void* out, int64_t begin, int64_t end,
+                                int32_t steps, uint32_t* counters, uint64_t* face_signal, uint32_t gate_need,
+                                uint32_t* release_flag, int32_t* signals_per_face, void* stream) {
+    if (int rc = check_layout(l)) return rc;
+    if (!counters) return set_error(STENCIL_EINVAL, "null counters");
+    if (begin < 0 || end > stencil_slow_extent(l) || begin > end)
+        return set_error(STENCIL_EINVAL, "sweep range out of bounds");
+    if (in == out) return set_error(STENCIL_EINVAL, "in-place sweeps are not supported");
+    if (box27_supports(l->prob)) return set_error(STENCIL_EUNSUPPORTED, "the halo-gated launch is the 7-point star's");
+    int nsig = 0;
+    StripGate gate;
+    gate.word = counters + 3;
+    gate.release = release_flag;
+    gate.need = gate_need;
+    const int rc = launch_tkstrip_signal(*l, in, out, begin, end, steps, counters,
+                                         reinterpret_cast<unsigned long long*>(face_signal), &nsig,
+                                         as_stream(stream), gate);
+    if (rc == STENCIL_OK) {
+        if (signals_per_face) *signals_per_face = nsig;
+        clear_error();
+    }
+    return rc;
+}
+
+int stencil_exchange_done(uint32_t* counters, uint32_t value, void* stream) {
+    clear_error();
+    if (!counters) return set_error(STENCIL_EINVAL, "null counters");
+    hipLaunchKernelGGL(exchange_done_kernel, dim3(1), dim3(64), 0, as_stream(stream), counters + 3, value);
+    STENCIL_LAUNCH_CHECK();
+    return STENCIL_OK;
 }
 
 int stencil_wait_counters(const uint32_t* counters, uint32_t target_lo, uint32_t target_hi, uint32_t* timeout_flag,

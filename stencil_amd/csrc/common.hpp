@@ -167,8 +167,19 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
 // machine scheduler (launch_tkstrip routes the shapes measured faster that way)
 int launch_tkstrip_ilp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                        hipStream_t s);
+// The halo gate of a face-signalled launch (stencil_sweepk_signal_gated):
+// the workgroups whose z range reaches a halo plane first wait until *word
+// (the slab's exchange-completion word, stencil_exchange_done) has reached
+// `need` (wrap-safe), or until *release != 0 (a failed job), or 10 s (then
+// it sets *release: the job reports the timeout).  A null word: no gate.
+struct StripGate {
+    const uint32_t* word = nullptr;
+    uint32_t* release = nullptr;
+    uint32_t need = 0;
+};
 int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
-                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s);
+                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s,
+                          const StripGate& gate = StripGate{});
 int launch_boxk(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                 hipStream_t s);
 int launch_boxk_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,

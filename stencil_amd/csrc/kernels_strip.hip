@@ -155,6 +155,31 @@ __device__ __forceinline__ void tier_spin(const uint32_t* p, uint32_t need, unsi
         __builtin_amdgcn_s_sleep(1);
     }
 }
+// The halo gate (SIG, StripGate): one lane polls the exchange-completion
+// word with relaxed agent-scope loads (they bypass L1) until it reaches
+// `need`, the host releases it (a failed job) or 10 s of s_memrealtime
+// (100 MHz) pass (then it sets the release flag, the job's timeout flag, so
+// run() reports the failure); then ONE agent acquire and its vmcnt wait, before the
+// workgroup barrier behind which every wave loads the halo planes
+// (MI355X_MICROARCH.md §visibility, the consumer recipe).  The word is written
+// by a one-lane kernel queued behind the exchange's transfers on their stream
+// (stencil_exchange_done), so the transfers' kernels have ended -- and
+// released their writes -- before it.
+__device__ __forceinline__ void gate_wait(const StripGate& g) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (int32_t(__hip_atomic_load(g.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - g.need) < 0) {
+        if (g.release && __hip_atomic_load(g.release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > uint64_t(1000) * 1000 * 1000) {
+            // the halos this chunk reads are stale: fail the job (as a face-counter wait does)
+            if (g.release) __hip_atomic_store(g.release, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <typename VT>
 __device__ __forceinline__ VT sc1_load(const void* p) {
     static_assert(sizeof(VT) == 8, "tier hand-offs move 8-byte lane vectors");
@@ -194,7 +219,7 @@ __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
                 unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast, int xcd_pw,
-                TierArgs tier) {
+                TierArgs tier, StripGate gate) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
@@ -409,6 +434,15 @@ __global__ void __launch_bounds__(64 * NW)
         // every producer in reach has stored it (and plane 0)
         if (tnb >= 0) tier_spin(tier_flags + tnb * kTierFlagStride, tier.base + 1u, tier.fail);
         __syncthreads();
+    }
+    if constexpr (SIG) {
+        // halo gate: a chunk whose loads reach a halo plane waits for the
+        // exchange that filled it (the launch follows the previous round's
+        // launch on its queue, with no event wait for that exchange)
+        if (gate.word && ((halo_lo && zfirst < 0) || (halo_hi && zlast >= nz))) {
+            if (threadIdx.x == 0 && threadIdx.y == 0) gate_wait(gate);
+            __syncthreads();
+        }
     }
 #pragma unroll
     for (int i = 0; i < NS - 2; ++i) load_plane(vin[i], p0 + i);
@@ -651,7 +685,8 @@ int senv_int(const char* name, int dflt) { return knob(name, dflt); }
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
           bool FP = true, bool HL = false>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
-              unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr) {
+              unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr,
+              const StripGate& gate = StripGate{}) {
     using Tl = StripTile<T, V, RY, NW, K, DB>;
     static_assert(Tl::lds_bytes + (HL ? size_t(2) * Tl::RH * Tl::RW * sizeof(T) : 0) <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
@@ -794,7 +829,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         hipLaunchKernelGGL(kern, dim3(unsigned(n)), dim3(64, NW, 1), 0, s,
                            static_cast<const T*>(in), static_cast<T*>(out), g, int(begin), int(end), zc, int(gx),
                            int(gy), int(lo), int(hi), avg_weight<T>(l.prob), sig, fsig, packed ? sched : nullptr,
-                           fast_of(packed), packed ? 0 : xcd_pw, TierArgs{});
+                           fast_of(packed), packed ? 0 : xcd_pw, TierArgs{}, SIG ? gate : StripGate{});
         return hipGetLastError();
     };
     if (sched && verdict && verdict->load() == kPackUntested) return pick_schedule(verdict, s, launch);
@@ -909,7 +944,7 @@ int tier_launch(const stencil_layout& l, const void* in, void* out, TierJob* j, 
     const int fast = 1;  // few tiles: the interior fast path pays (as the packed regime)
     hipLaunchKernelGGL(kern, dim3(unsigned(2 * j->tiles)), dim3(64, 8, 1), 0, s, static_cast<const double*>(in),
                        static_cast<double*>(out), g, 0, int(g.nz), 0, int(gx), int(gy), 0, 0,
-                       avg_weight<double>(l.prob), nullptr, nullptr, nullptr, fast, 0, j->a);
+                       avg_weight<double>(l.prob), nullptr, nullptr, nullptr, fast, 0, j->a, StripGate{});
     STENCIL_LAUNCH_CHECK();
     j->a.base += uint32_t(g.nz + 1);  // the flags end at base + nz + 1: the next launch's origin
     return STENCIL_OK;
@@ -1285,21 +1320,21 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
 
 // The default shapes with face signalling (stencil_sweepk_signal).
 int launch_tkstrip_signal(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
-                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s) {
+                          unsigned* sig, unsigned long long* fsig, int* nsig, hipStream_t s, const StripGate& gate) {
     if (!temporal2_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "face-signalled sweeps cover the 3D r=1 naive 7-point star only");
     if (l.prob.dtype == STENCIL_F32) {
         switch (steps) {
-        case 3: return launch_st<float, 4, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-        case 4: return launch_st<float, 2, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-        case 5: return launch_st<float, 2, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 3: return launch_st<float, 4, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
+        case 4: return launch_st<float, 2, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
+        case 5: return launch_st<float, 2, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
         default: break;
         }
     } else {
         switch (steps) {
-        case 3: return launch_st<double, 2, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-        case 4: return launch_st<double, 1, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
-        case 5: return launch_st<double, 1, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig);
+        case 3: return launch_st<double, 2, 4, 8, 3, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
+        case 4: return launch_st<double, 1, 7, 8, 4, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
+        case 5: return launch_st<double, 1, 5, 8, 5, true, 0, true>(l, in, out, begin, end, s, sig, nsig, fsig, gate);
         default: break;
         }
     }

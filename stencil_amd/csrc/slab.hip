@@ -351,6 +351,38 @@ struct HipDev {
     static int wait_counters(uint32_t* c, uint32_t* flag, uint32_t lo, uint32_t hi, Stream s) {
         return stencil_wait_counters(c, lo, hi, flag, s);
     }
+    // Halo-gated face-signalled launches (stencil_sweepk_signal_gated; the
+    // 7-point star): only where the workgroups that may wait for an exchange
+    // can never hold every CU the exchange's own kernels (RCCL's, the
+    // completion store) need -- a confined exchange has CUs of its own, and
+    // otherwise the waiting chunks (at most the two face chunks of every
+    // tile) must fit one round with a CU per XCD to spare, as the 512^3-class
+    // grids do (110 tiles: 220 <= 248).  STENCIL_SLAB_GATE=0: never.
+    static bool halo_gate(const stencil_layout& l, int k, bool confined) {
+        if (api_knob("STENCIL_SLAB_GATE", 1) == 0 || l.prob.shape != STENCIL_STAR) return false;
+        if (confined) return true;
+        int64_t tiles = 0, wg = 0;
+        int slots = 0;
+        if (signal_launch_geometry(l, 0, l.prob.nz, k, &tiles, &wg, &slots) != STENCIL_OK) {
+            clear_error();
+            return false;
+        }
+        return slots > 0 && 2 * tiles <= slots - slots / 32;
+    }
+    static int sweepk_signal_gated(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k,
+                                   uint32_t* counters, uint64_t* fsig, uint32_t need, uint32_t* release, int* nsig,
+                                   Stream s) {
+        int32_t n = 0;
+        // STENCIL_SLAB_GATE_SKIP=1 (debug library, the test that shows the
+        // gate has teeth): a need every word meets, so nothing waits
+        if (knob("STENCIL_SLAB_GATE_SKIP", 0)) need = 0;
+        const int rc = stencil_sweepk_signal_gated(l, src, dst, b, e, k, counters, fsig, need, release, &n, s);
+        *nsig = n;
+        return rc;
+    }
+    static int exchange_done(uint32_t* counters, uint32_t value, Stream s) {
+        return stencil_exchange_done(counters, value, s);
+    }
     static int read_timeout(uint32_t* flag, bool* timed_out) {
         *timed_out = __atomic_load_n(flag, __ATOMIC_SEQ_CST) != 0;
         return STENCIL_OK;
@@ -560,6 +592,10 @@ int stencil_slab_plane_sums(stencil_slab_job* job, double* sums) {
 
 int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form) {
     return core::round_form<HipDev>(job, form);
+}
+
+int stencil_slab_round_info(const stencil_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined) {
+    return core::round_info<HipDev>(job, form, gated, confined);
 }
 
 int stencil_slab_set_timeout(stencil_slab_job* job, int64_t timeout_ms) {

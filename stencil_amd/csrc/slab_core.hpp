@@ -82,6 +82,11 @@ struct Slab {
     // processor (hipStreamWaitValue64) instead of a polling wait kernel
     uint64_t* fsig = nullptr;
     uint64_t fsig_target = 0;
+    // halo-gated rounds (Job::gate): exchanges issued on X since the last
+    // reset; each one's completion stores its number in counters[3]
+    // (Dev::exchange_done), which the next launch's halo-reading workgroups
+    // wait for instead of the launch's queue waiting for X's event
+    uint32_t xseq = 0;
     // overlapped rolling rounds: the new grid's faces are computed into the
     // send staging xs and travel from there while the pass runs; the
     // neighbours' faces land in the receive staging xr and are copied into
@@ -108,6 +113,12 @@ struct Job {
     bool cur_is_a = true;
     bool chained = false;  // round events recorded since the last join
     bool signal = false;   // full rounds as face-signalled single launches
+    // face-signalled rounds whose launches gate their halo-reading workgroups
+    // on the exchange-completion word (Dev::halo_gate): the launch queue never
+    // waits for the exchange queue; gate_chain = the last round issued was
+    // such a launch, so the next one may skip the event wait
+    bool gate = false;
+    bool gate_chain = false;
     bool serial = false;   // full rounds as ONE plain launch, then the exchange (STENCIL_SLAB_SERIAL)
     int nranks = 0;        // rank mode: slabs of the job, this process owns s[0]
     // rolling (STENCIL_SLAB_ROLLING): spare planes below each slab's grid;
@@ -323,6 +334,7 @@ int exchange(Job<Dev>& j, int pos, Pre&& pre = Pre{}) {
         SLAB_TRY(Dev::set_device(s.device));
         if (j.tuning) SLAB_TRY(Dev::event_record(s.tx1, s.sx));
         SLAB_TRY(xspan_end(j, s));
+        if (j.gate) SLAB_TRY(Dev::exchange_done(s.counters, ++s.xseq, s.sx));
         SLAB_TRY(Dev::event_record(s.ev_xout, s.sx));
     }
     for (int i = 0; i < n; ++i) {
@@ -410,13 +422,22 @@ int slab_round_signal(Job<Dev>& j, int k) {
         SLAB_TRY(Dev::set_device(s.device));
         void* src = grid_at(j, s, src_pos);
         void* dst = grid_at(j, s, dst_pos);
-        // the launch reads the halos the last exchange received: wait for X
-        // directly (through A, ev_bnd, costs a third queue hop per round:
-        // ~20 us of 500 at 512^3)
-        if (j.chained) SLAB_TRY(Dev::stream_wait(s.sb, s.ev_xout));
+        // the launch reads the halos the last exchange received.  Gated
+        // rounds: its halo-reading workgroups wait for that exchange's
+        // completion word, and the launch follows the previous round's gated
+        // launch on B with no event wait -- that launch's own gated workgroups
+        // saw the exchange before it (the grid this launch writes) complete
+        // (the cross-queue wait cost ~23 us of a 0.49 ms round at 512^3,
+        // DESIGN.md §7).  Otherwise wait for X directly (through A, ev_bnd,
+        // costs a third queue hop per round: ~20 us of 500 at 512^3)
+        if (j.chained && !(j.gate && j.gate_chain)) SLAB_TRY(Dev::stream_wait(s.sb, s.ev_xout));
         int nsig = 0;
         SLAB_TRY(time_begin(j, i, s.sb));
-        SLAB_TRY(Dev::sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, s.fsig, &nsig, s.sb));
+        if (j.gate)
+            SLAB_TRY(Dev::sweepk_signal_gated(&s.l, src, dst, 0, s.n, k, s.counters, s.fsig, s.xseq, s.tflag, &nsig,
+                                              s.sb));
+        else
+            SLAB_TRY(Dev::sweepk_signal(&s.l, src, dst, 0, s.n, k, s.counters, s.fsig, &nsig, s.sb));
         SLAB_TRY(time_end(j, i, s.sb, s.l.prob.nx * s.l.prob.ny * s.n, 1));
         SLAB_TRY(Dev::event_record(s.ev_int, s.sb));
         s.sig_target += uint32_t(nsig);
@@ -436,6 +457,7 @@ int slab_round_signal(Job<Dev>& j, int k) {
         SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
     }
     j.chained = true;
+    j.gate_chain = j.gate;
     j.cur_is_a = dst_pos == 0;
     return STENCIL_OK;
 }
@@ -733,6 +755,7 @@ int sync_bounded(Job<Dev>& j) {
             if (int rc = Dev::sync_until(st, s.comm, deadline)) return fail(j, rc);
     }
     j.chained = false;
+    j.gate_chain = false;
     return STENCIL_OK;
 }
 
@@ -952,6 +975,9 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
                 j->staged = true;
                 j->signal = false;
             }
+            // halo-gated launches where a waiting workgroup can never hold
+            // the CU the exchange's kernels need (Dev::halo_gate)
+            if (j->signal) j->gate = Dev::halo_gate(l, j->k, j->confine);
         }
     }
     j->timeout_ms = Dev::default_timeout_ms();
@@ -1167,6 +1193,7 @@ int reset_signals(Job<Dev>& j) {
         SLAB_TRY(Dev::reset_counters(s.counters, s.tflag, s.fsig));
         s.sig_target = 0;
         s.fsig_target = 0;
+        s.xseq = 0;
     }
     return STENCIL_OK;
 }
@@ -1206,25 +1233,38 @@ int fill_initial(JobT* job, int32_t init_kind, uint64_t seed) {
 // ghost cell, and a pass lands plane z of the new grid in a slot whose ring
 // came from an older plane or from the margin's copies of plane -1.  The
 // reference initial condition has this; an uploaded grid must too.
+// Host planes [z0, z1) (host plane index = global plane + r) are compared
+// with ONE anchor, plane z0: the ring cells of every plane, and every cell of
+// the global bottom ghost planes (host planes < r).  Only ring cells are
+// visited: full rows y < r and y >= ny + r, the x < r / x >= nx + r ends of
+// the others (the 4096^3 grids this form exists for have 2^24 interior cells
+// a plane).
 template <class T>
-int check_rolling_rings(const T* h, const stencil_problem& g, int64_t row, int64_t rows) {
-    const int64_t r = g.radius, w = g.nx + 2 * r, hgt = g.ny + 2 * r, planes = g.nz + 2 * r;
+int check_rolling_rings(const T* h, const stencil_problem& g, int64_t row, int64_t rows, int64_t z0, int64_t z1) {
+    const int64_t r = g.radius, w = g.nx + 2 * r, hgt = g.ny + 2 * r;
     const size_t hp = size_t(row) * size_t(rows);
-    auto ring_cell = [&](int64_t y, int64_t x) { return y < r || y >= g.ny + r || x < r || x >= g.nx + r; };
-    for (int64_t z = 1; z < planes; ++z)
-        for (int64_t y = 0; y < hgt; ++y)
-            for (int64_t x = 0; x < w; ++x) {
-                if (!ring_cell(y, x) && !(z < r)) continue;  // bottom ghost planes: every cell
-                const T a = h[size_t(z) * hp + size_t(y * row + x)];
-                const T b = h[(z < r ? size_t(r - 1) * hp : 0) + size_t(y * row + x)];
-                if (std::memcmp(&a, &b, sizeof(T)) != 0)
-                    return set_error(STENCIL_EINVAL,
-                                     "rolling slab upload: host plane %lld cell (x %lld, y %lld) differs from %s -- "
-                                     "rolling slabs need the same x/y ghost ring in every plane and equal bottom "
-                                     "ghost planes (use two grids: no STENCIL_SLAB_ROLLING)",
-                                     (long long)(z - r), (long long)(x - r), (long long)(y - r),
-                                     z < r ? "ghost plane -1" : "the ring of ghost plane -r");
+    const T* anchor = h + size_t(z0) * hp;
+    auto cmp = [&](int64_t z, int64_t y, int64_t x) {
+        const T a = h[size_t(z) * hp + size_t(y * row + x)];
+        const T b = anchor[size_t(y * row + x)];
+        if (std::memcmp(&a, &b, sizeof(T)) == 0) return STENCIL_OK;
+        return set_error(STENCIL_EINVAL,
+                         "rolling slab upload: host plane %lld cell (x %lld, y %lld) differs from plane %lld -- "
+                         "rolling slabs need the same x/y ghost ring in every plane and equal bottom "
+                         "ghost planes (use two grids: no STENCIL_SLAB_ROLLING)",
+                         (long long)(z - r), (long long)(x - r), (long long)(y - r), (long long)(z0 - r));
+    };
+    for (int64_t z = z0 + 1; z < z1; ++z) {
+        const bool full = z < r;  // a global bottom ghost plane: every cell
+        for (int64_t y = 0; y < hgt; ++y) {
+            if (full || y < r || y >= g.ny + r) {
+                for (int64_t x = 0; x < w; ++x) SLAB_TRY(cmp(z, y, x));
+            } else {
+                for (int64_t x = 0; x < r; ++x) SLAB_TRY(cmp(z, y, x));
+                for (int64_t x = g.nx + r; x < w; ++x) SLAB_TRY(cmp(z, y, x));
             }
+        }
+    }
     return STENCIL_OK;
 }
 
@@ -1235,9 +1275,12 @@ int upload(JobT* job, const void* host, int64_t host_row, int64_t host_rows) {
     if (host_row < g.nx + 2 * g.radius || host_rows < g.ny + 2 * g.radius)
         return set_error(STENCIL_EINVAL, "host array too small");
     if (job->margin) {
+        // every rank checks the whole global array (ring cells only), so a bad
+        // grid fails every rank alike, before any exchange
+        const int64_t z1 = g.nz + 2 * g.radius;
         const int rc = g.dtype == STENCIL_F64
-                           ? check_rolling_rings(static_cast<const double*>(host), g, host_row, host_rows)
-                           : check_rolling_rings(static_cast<const float*>(host), g, host_row, host_rows);
+                           ? check_rolling_rings(static_cast<const double*>(host), g, host_row, host_rows, 0, z1)
+                           : check_rolling_rings(static_cast<const float*>(host), g, host_row, host_rows, 0, z1);
         SLAB_TRY(rc);
     }
     SLAB_TRY(sync_bounded(*job));
@@ -1265,6 +1308,7 @@ int upload(JobT* job, const void* host, int64_t host_row, int64_t host_rows) {
 template <class Dev>
 int one_round(Job<Dev>& j, int k, bool full) {
     SLAB_TRY(throttle(j));
+    if (!(full && j.signal)) j.gate_chain = false;  // only a gated launch may follow a gated launch unsynchronised
     if (j.margin)
         SLAB_FAIL(j, j.roll_overlap ? slab_round_rolling_overlap(j, k) : slab_round_rolling(j, k));
     else if (full && j.signal)
@@ -1412,6 +1456,15 @@ template <class Dev, class JobT>
 int round_form(const JobT* job, int32_t* form) {
     if (!job || !form) return set_error(STENCIL_EINVAL, "null argument");
     *form = round_form_of(*job);
+    return STENCIL_OK;
+}
+
+template <class Dev, class JobT>
+int round_info(const JobT* job, int32_t* form, int32_t* gated, int32_t* confined) {
+    if (!job) return set_error(STENCIL_EINVAL, "null job");
+    if (form) *form = round_form_of(*job);
+    if (gated) *gated = job->signal && job->gate ? 1 : 0;
+    if (confined) *confined = job->confine ? 1 : 0;
     return STENCIL_OK;
 }
 

@@ -533,6 +533,15 @@ class SlabJob:
         _lib.check(self.lib.stencil_slab_round_form(self.job, ctypes.byref(f)), "stencil_slab_round_form", lib=self.lib)
         return int(f.value)
 
+    def round_info(self) -> dict:
+        """The form plus whether face-signalled launches are halo-gated (no
+        event wait between rounds) and whether the exchange is confined to
+        CUs of its own (stencil_slab_round_info)."""
+        f, g, c = ctypes.c_int32(-1), ctypes.c_int32(0), ctypes.c_int32(0)
+        _lib.check(self.lib.stencil_slab_round_info(self.job, ctypes.byref(f), ctypes.byref(g), ctypes.byref(c)),
+                   "stencil_slab_round_info", lib=self.lib)
+        return {"form": int(f.value), "gated": bool(g.value), "confined": bool(c.value)}
+
     def set_timeout(self, ms: int) -> None:
         """The job's deadline for every device wait (stencil_slab_set_timeout):
         past it the job fails with STENCIL_ETIMEOUT and aborts its communicators."""

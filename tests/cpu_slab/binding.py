@@ -35,6 +35,7 @@ class FakeSlabLib:
         cdll.fake_slab_set_signal.argtypes = [ctypes.c_int32]
         cdll.fake_slab_set_free_bytes.argtypes = [ctypes.c_int64]
         cdll.fake_slab_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+        cdll.fake_slab_gate_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
         cdll.fake_slab_layout_init.argtypes = [ctypes.POINTER(_lib.Problem), ctypes.POINTER(_lib.Layout)]
 
     # what _lib.check calls on failure
@@ -68,6 +69,14 @@ class FakeSlabLib:
         out = (ctypes.c_int64 * 5)()
         self._cdll.fake_slab_stats(out, 1 if reset else 0)
         return dict(zip(("sweeps", "signal_sweeps", "sends", "recvs", "peer_copies"), list(out)))
+
+    def gate_stats(self, reset: bool = False) -> dict:
+        """Halo-gated launches, gate numbering violations (a launch whose
+        awaited exchange number is not the last completed one, an exchange
+        completion out of order) and exchange-completion stores."""
+        out = (ctypes.c_int64 * 3)()
+        self._cdll.fake_slab_gate_stats(out, 1 if reset else 0)
+        return dict(zip(("gated", "violations", "completions"), list(out)))
 
 
 def available() -> bool:

@@ -77,6 +77,7 @@ bool g_signal = true;                 // face-signalled rounds allowed
 int64_t g_free = int64_t(1) << 40;    // "device" free bytes (rolling margin from memory)
 std::mutex g_stat_mu;
 int64_t g_sweeps = 0, g_signal_sweeps = 0, g_sends = 0, g_recvs = 0, g_peer_copies = 0;
+int64_t g_gated = 0, g_gate_bad = 0, g_xdone = 0;  // gated launches, numbering violations, completion stores
 
 struct Event {
     std::chrono::steady_clock::time_point t{};
@@ -383,6 +384,31 @@ struct FakeDev {
         *nsig = 1;
         return STENCIL_OK;
     }
+    // halo-gated launches (FAKE_SLAB_GATE=0: off): the fake's streams are
+    // synchronous, so the exchange a gated launch waits for has completed
+    // when the launch is issued -- unless the core's exchange numbering is
+    // wrong, which counts as a violation (on a GPU: a launch that waits for
+    // an exchange that never comes, or reads halos too early)
+    static bool halo_gate(const stencil_layout&, int, bool) {
+        const char* v = std::getenv("FAKE_SLAB_GATE");
+        return !(v && *v && std::atoi(v) == 0);
+    }
+    static int sweepk_signal_gated(const stencil_layout* l, const void* src, void* dst, int64_t b, int64_t e, int k,
+                                   uint32_t* counters, uint64_t* fsig, uint32_t need, uint32_t*, int* nsig, Stream s) {
+        {
+            std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+            ++fake::g_gated;
+            if (int32_t(counters[3] - need) < 0 || counters[3] != need) ++fake::g_gate_bad;
+        }
+        return sweepk_signal(l, src, dst, b, e, k, counters, fsig, nsig, s);
+    }
+    static int exchange_done(uint32_t* counters, uint32_t value, Stream) {
+        std::lock_guard<std::mutex> lk(fake::g_stat_mu);
+        if (value != counters[3] + 1) ++fake::g_gate_bad;  // one completion per exchange, in order
+        counters[3] = value;
+        ++fake::g_xdone;
+        return STENCIL_OK;
+    }
     static int wait_counters(uint32_t* c, uint32_t* flag, uint32_t lo, uint32_t hi, Stream) {
         if (c[0] < lo || c[1] < hi) *flag = 1;  // synchronous: a count short now never arrives
         return STENCIL_OK;
@@ -586,6 +612,18 @@ void fake_slab_stats(int64_t* out5, int32_t reset) {
     if (reset) g_sweeps = g_signal_sweeps = g_sends = g_recvs = g_peer_copies = 0;
 }
 
+// gated launches, gate numbering violations, exchange-completion stores since the last reset
+void fake_slab_gate_stats(int64_t* out3, int32_t reset) {
+    std::lock_guard<std::mutex> lk(stencil::fake::g_stat_mu);
+    using namespace stencil::fake;
+    if (out3) {
+        out3[0] = g_gated;
+        out3[1] = g_gate_bad;
+        out3[2] = g_xdone;
+    }
+    if (reset) g_gated = g_gate_bad = g_xdone = 0;
+}
+
 int fake_slab_create(const stencil_problem* g, int32_t n, const int32_t* devs, int32_t ex, int32_t flags,
                      fake_slab_job** job) {
     return core::create<FakeDev>(g, n, devs, ex, flags, 0, job);
@@ -640,6 +678,9 @@ int fake_slab_plane_sums(fake_slab_job* job, double* sums) { return core::plane_
 // the fake's layout arithmetic, compared with the product's stencil_layout_init
 int fake_slab_layout_init(const stencil_problem* p, stencil_layout* out) { return FakeDev::layout_init(p, out); }
 int fake_slab_round_form(const fake_slab_job* job, int32_t* form) { return core::round_form<FakeDev>(job, form); }
+int fake_slab_round_info(const fake_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined) {
+    return core::round_info<FakeDev>(job, form, gated, confined);
+}
 int fake_slab_set_timeout(fake_slab_job* job, int64_t ms) { return core::set_timeout<FakeDev>(job, ms); }
 
 }  // extern "C"

@@ -166,13 +166,16 @@ def test_product_library_ignores_experiment_knobs(monkeypatch):
 def test_row_pitch_rule():
     """stencil_layout_init's row-pitch rule: pitches of
     32 KiB or more within [-512, +256] B of a multiple of 32 KiB move to
-    residue 384 (from [0, 256]) or 128 B up (from [-512, -128]); every other
+    residue 384 (from [-256, 256]) or 128 B up (from [-512, -384]); every other
     pitch is the 128-B-aligned minimum.  Every preset width is covered."""
     from stencil_amd import _lib
     cases = {  # (dtype, nx): row pitch in bytes
         ("fp64", 512): 4352, ("fp64", 2048): 16640, ("fp32", 4096): 16640,  # C2, C4/C5/NS, C3: no padding
         ("fp64", 4096): 33152,   # NS4096: 33024 (r 256) -> 33152
         ("fp64", 4000): 32384,   # 32256 (r -512) -> +128
+        ("fp64", 4032): 33152,   # 32512 (r -256) -> r 384 (ADVICE r05: +128 would land on r -128)
+        ("fp64", 4048): 33152,   # 32640 (r -128) -> r 384 (+128 would land on r 0)
+        ("fp32", 8112): 33152,   # 32640 (r -128) -> r 384
         ("fp64", 4128): 33280,   # r 512: unpadded
         ("fp64", 8160): 65920,   # 65536 (r 0) -> r 384
         ("fp64", 8192): 65920,   # 65792 (r 256) -> r 384

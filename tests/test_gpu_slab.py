@@ -498,8 +498,10 @@ def test_staged_rounds_match_boundary_launches(gpu, monkeypatch, shape, dtype, e
     """STAGED rounds, AUTO's form for slabs whose launch takes several rounds
     of workgroups (2048 x 1024 planes): the face quarters on every CU, then
     the middle on the CUs the confined exchange leaves; remainders after the
-    full rounds -- bitwise the boundary + interior rounds."""
-    nx, ny, nz, it = 2048, 1024, 44, 11
+    full rounds -- bitwise the boundary + interior rounds.  21 sweeps: the
+    two tuning rounds, then at least two rounds with the TUNED face span
+    (11 sweeps never ran one)."""
+    nx, ny, nz, it = 2048, 1024, 44, 21
     want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False, dtype=dtype, shape=shape)
     monkeypatch.delenv("STENCIL_SLAB_SIGNAL", raising=False)
     monkeypatch.delenv("STENCIL_SLAB_STAGED", raising=False)
@@ -608,3 +610,73 @@ def test_exchange_time_beside_the_launch(gpu, monkeypatch, form):
             assert frac < 0.05, xt
     finally:
         job.close()
+
+
+def _gated_ring(gpu, monkeypatch, env, nx=130, ny=64, nz=40, it=17):
+    """One periodic slab, device-copy halos, face-signalled rounds with the
+    given environment: (round_info, final grid)."""
+    monkeypatch.setenv("STENCIL_SLAB_SIGNAL", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, nx, ny, nz, [gpu], exchange="copy", periodic=True)
+    try:
+        info = job.round_info()
+        job.fill_initial("random", 5)
+        job.run(it)
+        return info, job.download()
+    finally:
+        job.close()
+
+
+@pytest.mark.parametrize("exchange", ["copy", "rccl"])
+def test_gated_rounds_match_boundary_launches(gpu, monkeypatch, exchange):
+    """Halo-gated face-signalled rounds (the default for one-round grids such
+    as C2's 512^3 slab): the launch follows the previous launch on its queue
+    with no event wait for the exchange; only its halo-reading workgroups
+    wait for the exchange-completion word.  Bitwise the boundary + interior
+    rounds, over copies and RCCL to itself, through remainder rounds."""
+    nx, ny, nz, it = 130, 64, 40, 17
+    want = _periodic_job(gpu, monkeypatch, nx, ny, nz, it, False)
+    monkeypatch.setenv("STENCIL_SLAB_SIGNAL", "1")
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, nx, ny, nz, [gpu], exchange=exchange, periodic=True)
+    try:
+        assert job.round_info() == {"form": 1, "gated": True, "confined": False}
+        job.fill_initial("random", 5)
+        job.run(it - 5)
+        job.run(5)  # continued calls: the first round after a sync waits on nothing, gated all the same
+        got = job.download()
+    finally:
+        job.close()
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+def test_gated_rounds_slow_exchange(gpu, monkeypatch):
+    """A 3 ms spin before every exchange's copies (STENCIL_SLAB_COPY_DELAY_US,
+    debug library): each launch's halo-reading chunks must wait for the
+    previous exchange's completion word.  Bitwise the boundary + interior
+    rounds."""
+    want = _periodic_job(gpu, monkeypatch, 130, 64, 40, 17, False)
+    info, got = _gated_ring(gpu, monkeypatch, {"STENCIL_SLAB_COPY_DELAY_US": "3000"})
+    assert info["gated"] and info["form"] == 1
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+def test_gated_rounds_slow_exchange_need_the_gate(gpu, monkeypatch):
+    """The test above has teeth: with the gate's need forced to 0
+    (STENCIL_SLAB_GATE_SKIP, debug library) nothing orders a launch after the
+    slow exchange, and the halos it reads are stale."""
+    want = _periodic_job(gpu, monkeypatch, 130, 64, 40, 17, False)
+    info, got = _gated_ring(gpu, monkeypatch, {"STENCIL_SLAB_COPY_DELAY_US": "3000", "STENCIL_SLAB_GATE_SKIP": "1"})
+    assert info["gated"]
+    assert not np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+def test_gate_off_waits_for_the_exchange_event(gpu, monkeypatch):
+    """STENCIL_SLAB_GATE=0: the face-signalled rounds of round 5 (the launch
+    waits for the exchange stream's event), bitwise the same."""
+    want = _periodic_job(gpu, monkeypatch, 130, 64, 40, 17, False)
+    info, got = _gated_ring(gpu, monkeypatch, {"STENCIL_SLAB_GATE": "0", "STENCIL_SLAB_COPY_DELAY_US": "3000"})
+    assert not info["gated"] and info["form"] == 1
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))

@@ -434,6 +434,36 @@ def test_upload_checks_the_rolling_ghost_ring(fake):
     two.close()
 
 
+@pytest.mark.parametrize("where", ["interior of ghost plane -2", "ring of ghost plane -1", "ring of plane 5",
+                                   "interior of top ghost plane"])
+def test_upload_checks_the_rolling_ghost_ring_radius_two(fake, where):
+    """with r = 2 the bottom ghost planes -2 and -1 must
+    be equal in every cell and every plane's ring must equal plane -2's ring;
+    the check used plane r - 1 as its own reference and never compared plane
+    -2.  A top ghost plane's interior is not constrained (no pass moves it
+    into another plane's slot)."""
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star", radius=2)
+    nx, ny, nz = 9, 6, 12
+    p2 = ob.problem(3, "fp64", "star", 2, "naive", nx, ny, nz)
+    good = ob.init(p2, "random", 5)
+    bad = good.copy()
+    # host index = plane + 2, row + 2, column + 2
+    z, y, x = {"interior of ghost plane -2": (0, 4, 5), "ring of ghost plane -1": (1, 0, 5),
+               "ring of plane 5": (7, 3, 1), "interior of top ghost plane": (nz + 3, 4, 5)}[where]
+    bad[z, y, x] = 0.5
+    job = SlabJob(spec, nx, ny, nz, [0, 1], exchange="rccl", rolling=True, margin=12, lib=fake)
+    try:
+        job.upload(good)
+        if where == "interior of top ghost plane":
+            job.upload(bad)
+        else:
+            with pytest.raises(_lib.StencilError, match="same x/y ghost ring"):
+                job.upload(bad)
+    finally:
+        job.close()
+
+
 @pytest.mark.parametrize("case,form", [
     (dict(devs=[0, 1]), 1),                      # distinct devices: face-signalled
     (dict(devs=[0, 0], exchange="copy"), 0),     # shared: boundary + interior
@@ -526,3 +556,46 @@ def test_staged_rank_mode_equals_one_grid(fake, monkeypatch, nranks):
         z1 = inf["first"] + inf["planes"] + (1 if r == nranks - 1 else 0)
         got[z0 + 1:z1 + 1] = dense[z0 + 1:z1 + 1]
     assert_bitwise(got, want)
+
+
+@pytest.mark.parametrize("nslabs", [1, 2, 3])
+@pytest.mark.parametrize("exchange", ["rccl", "copy"])
+@pytest.mark.parametrize("gate", [True, False])
+def test_gated_rounds_number_their_exchanges(fake, monkeypatch, nslabs, exchange, gate):
+    """Halo-gated face-signalled rounds (round 6): every exchange stores its
+    number in the slab's completion word, and every gated launch waits for
+    the number of the last exchange issued before it -- on the fake's
+    synchronous streams that exchange is complete when the launch is issued,
+    so any other number is a violation (on a GPU: a launch waiting for an
+    exchange that never comes, or reading halos too early).  Full and
+    remainder rounds, continued calls, a refill in between; bitwise one grid.
+    FAKE_SLAB_GATE=0: the event-waiting rounds, no completion stores."""
+    if not gate:
+        monkeypatch.setenv("FAKE_SLAB_GATE", "0")
+    k = 4
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 11, 7, 3 * k * nslabs + 1
+    job = SlabJob(spec, nx, ny, nz, list(range(nslabs)), exchange=exchange, lib=fake)
+    try:
+        assert job.round_info() == {"form": 1, "gated": gate, "confined": False}
+        fake.gate_stats(reset=True)
+        job.fill_initial("random", 3)
+        sweeps = rounds = 0
+        for it in (2 * k + 1, k, 3, 2 * k):
+            job.run(it)
+            sweeps += it
+            rounds += it // k + (1 if it % k else 0)
+        st = fake.gate_stats()
+        full = sum(it // k for it in (2 * k + 1, k, 3, 2 * k))
+        assert st["violations"] == 0, st
+        assert st["gated"] == (full * nslabs if gate else 0), st
+        # fill: two exchanges (both grids), then one per round, on every slab
+        assert st["completions"] == ((2 + rounds) * nslabs if gate else 0), st
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, sweeps, seed=3))
+        job.fill_initial("random", 3)  # the numbering restarts with the counters
+        job.run(k)
+        assert fake.gate_stats()["violations"] == 0
+        assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, k, seed=3))
+    finally:
+        job.close()

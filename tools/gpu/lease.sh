@@ -208,6 +208,25 @@ for step in "$@"; do
           done ;;
     cumask) /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/cumask_probe.hip -o /tmp/cumask_probe &&
             timeout -k 10 60 /tmp/cumask_probe > "$O/cumask_probe.txt" 2>&1 ;;
+    sustained) # the C2 job's sustained-load slowdown: telemetry (amdsmi, in-process) + a kernel trace, then a
+          # GRBM_GUI_ACTIVE pass (cycles per launch), then the probe with no profiler at all
+          (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/sust_trace" \
+             -o run -- python3 "$R/tools/sustained_probe.py" --out "$O/sustained_trace.json" > "$O/sustained_trace.log" 2>&1) &&
+          (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE --output-format csv \
+             -d "$O/sust_pmc" -o run -- python3 "$R/tools/sustained_probe.py" --out "$O/sustained_pmc.json" \
+             > "$O/sustained_pmc.log" 2>&1) &&
+          timeout -k 10 200 python3 tools/sustained_probe.py --out "$O/sustained_plain.json" > "$O/sustained_plain.log" 2>&1 ;;
+    placeab) # bench.py --steps 1000 with 1 and 16 grid placements, alternating, three runs each
+          for rep in 1 2 3; do
+            for p in 1 16; do
+              timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --placements $p --no-cpu-baseline \
+                > "$O/bench_1000_place${p}_$rep.json" 2>> "$O/bench.err" || exit 1
+            done
+          done ;;
+    sqlib:*) # sqlib:<dtype>:nx:ny:nz:sweeps -- SQ / LDS / TCC counter passes of AUTO's launches of one shape
+          IFS=':' read -r dt nx ny nz sw <<< "${step#sqlib:}"
+          PROG=tools/time_lib.py bash profiles/collect_sq.sh "${TAG}_${dt}_${nx}x${ny}x${nz}" \
+            stencil_amd/libstencil_hip.so star "$dt" "$nx" "$ny" "$nz" "$sw" 1 > "$O/sq_${dt}_${nx}x${ny}x${nz}.log" 2>&1 ;;
     tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
              --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
