@@ -333,6 +333,14 @@ int stencil_rolling_iterate(const stencil_layout* l, void* base, int64_t shift_p
  * then times both grids on a shape's first launch (STENCIL_TK_PACK=1). */
 int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,
                       int64_t* equal_steps, int64_t* packed_steps, int64_t* workgroups);
+/* The packed grid itself (host only): {tile, first plane, planes} per
+ * workgroup in dispatch order, for a tile grid `tiles_x` wide; xcd_width > 0
+ * reorders every generation of equal chunks into XCD patches of that width
+ * (the dispatcher deals workgroup i to XCD i % 8).  Writes at most
+ * `capacity` triples into `table` (may be NULL) and the count to
+ * *workgroups (0: no packed grid). */
+int stencil_pack_table(int64_t tiles, int64_t tiles_x, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,
+                       int32_t xcd_width, int32_t* table, int64_t capacity, int64_t* workgroups);
 
 /* Launch plan of stencil_iterate for `iterations`: number of kernel launches
  * and the kernel family AUTO resolves to. */
@@ -471,6 +479,15 @@ int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form);
  * (stencil_sweepk_signal_gated; STENCIL_SLAB_GATE=0: never), *confined = 1
  * when the exchange runs on a few CUs of its own (STENCIL_SLAB_XCU). */
 int stencil_slab_round_info(const stencil_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined);
+/* The exchange's CU budget (staged rounds with a confined exchange, slab 0):
+ * CUs per XCD in use, the alternative budget the tuning rounds tried (0:
+ * none; STENCIL_SLAB_XCU_ALT, default 4), and the timed tuning round with the
+ * default (STENCIL_SLAB_XCU) and with the alternative budget, ms (0: not run:
+ * the alternative is tried only when the exchange ran at least 0.8x as long
+ * as the middle launch beside it).  The faster is kept (the alternative only
+ * when 2 % faster); the face span is then tuned from that round. */
+int stencil_slab_exchange_budget(const stencil_slab_job* job, int32_t* cus, int32_t* alt_cus, float* round_ms,
+                                 float* alt_round_ms);
 /* Bounded-time failure.  Every wait of the job for its devices (the end of
  * run(), fill, upload, download, plane sums, and -- while run() issues
  * rounds -- the exchange of the round kInflight = 8 rounds back) gives up

@@ -19,7 +19,7 @@ DEBUG_LIB_PATH = os.path.join(_HERE, "libstencil_hip_debug.so")
 API_KNOBS = ("STENCIL_TK_STEPS", "STENCIL_BOX_STEPS", "STENCIL_TK_PACK", "STENCIL_BOXK_PACK", "STENCIL_SLAB_SIGNAL",
              "STENCIL_SLAB_CPWAIT", "STENCIL_SLAB_SERIAL", "STENCIL_SLAB_XCU", "STENCIL_SLAB_XCU_EXCL",
              "STENCIL_SLAB_TIMEOUT_MS", "STENCIL_SLAB_ROLLING_OVERLAP", "STENCIL_SLAB_STAGED", "STENCIL_SLAB_GATE",
-             "STENCIL_SLAB_PLACEMENTS")
+             "STENCIL_SLAB_PLACEMENTS", "STENCIL_SLAB_XCU_ALT")
 
 STENCIL_OK = 0
 ETIMEOUT = -6
@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = (
     "stencil_slab_kernel_timing", "stencil_slab_kernel_time", "stencil_slab_unique_id", "stencil_slab_create_rank",
     "stencil_slab_create2", "stencil_slab_create_rank2", "stencil_slab_rolling_info", "stencil_slab_round_form",
     "stencil_slab_set_timeout", "stencil_prepare2", "stencil_slab_exchange_time",
-    "stencil_sweepk_signal_gated", "stencil_exchange_done", "stencil_slab_round_info",
+    "stencil_sweepk_signal_gated", "stencil_exchange_done", "stencil_slab_round_info", "stencil_pack_table",
+    "stencil_slab_exchange_budget",
 )
 
 
@@ -157,6 +158,8 @@ def signatures() -> dict:
                                             POINTER(c_int64), POINTER(c_float)]),
         "stencil_pack_plan": (c_int, [c_int64, c_int64, c_int32, c_int32, c_int32, POINTER(c_int64),
                                       POINTER(c_int64), POINTER(c_int64)]),
+        "stencil_pack_table": (c_int, [c_int64, c_int64, c_int64, c_int32, c_int32, c_int32, c_int32, POINTER(c_int32),
+                                       c_int64, POINTER(c_int64)]),
         "stencil_plan": (c_int, [L, c_uint32, POINTER(c_int64), POINTER(c_int32)]),
         "stencil_plane_sums": (c_int, [L, c_void_p, POINTER(c_double), c_void_p]),
         "stencil_copy_bandwidth": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, POINTER(c_float)]),
@@ -196,6 +199,8 @@ def signatures() -> dict:
                                              POINTER(c_int32)]),
         "stencil_slab_round_form": (c_int, [c_void_p, POINTER(c_int32)]),
         "stencil_slab_round_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+        "stencil_slab_exchange_budget": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_float),
+                                                 POINTER(c_float)]),
         "stencil_slab_set_timeout": (c_int, [c_void_p, c_int64]),
         "stencil_slab_exchange_time": (c_int, [c_void_p, POINTER(c_float), POINTER(c_float), POINTER(c_int64)]),
     }

@@ -106,9 +106,16 @@ extern const int* const kDrySchedule;
 // marching down (planes < 0 in the table), the short remainder in between,
 // so both faces lie in chunks of the first dispatch round; no table unless a
 // tile has at least 3 chunks.
+// xcd_w > 0 (tiles_x: the tile grid's width): within every generation of
+// equal chunks (same length and first plane) the table's entries are
+// reordered so that the workgroups the dispatcher deals to one XCD
+// (workgroup i -> XCD i % 8) hold a compact 2D patch of tiles -- column
+// strips of xcd_w tiles cut into 8 runs -- and neighbouring tiles' shared
+// halo lines become hits in that XCD's L2 (xcd_patch_order).  Same lengths
+// at the same positions: the same makespan.
 int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
                     hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict = nullptr,
-                    bool faces_out = false);
+                    bool faces_out = false, int64_t tiles_x = 0, int xcd_w = 0);
 
 // The dispatcher model behind packed_schedule mispredicts some shapes badly
 // (measured: 504 x 512 x 512 fp64 packed 0.555 vs equal 0.450 ms per launch,

@@ -781,8 +781,11 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         // STENCIL_TK_SIG_SPARE (debug library): CUs per XCD the packed
         // face-signalled schedule leaves to the exchange (default 1)
         const int pslots = SIG ? slots - slots / 32 * senv_int("STENCIL_TK_SIG_SPARE", 1) : slots;
+        // STENCIL_TK_PACK_XCD (debug library): the packed table's generations
+        // in XCD patches this many tiles wide (0: tile-major)
+        const int pack_xcd = senv_int("STENCIL_TK_PACK_XCD", 0);
         const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, pslots, zc, s,
-                                       tl_dry_launch != nullptr, &sched, &nb, &verdict, SIG);
+                                       tl_dry_launch != nullptr, &sched, &nb, &verdict, SIG, gx, pack_xcd);
         if (rc != STENCIL_OK) return rc;
         if (pack_mode != 1 || SIG) verdict = nullptr;  // 2: the model's choice, unmeasured
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
@@ -1087,9 +1090,36 @@ static bool faces_outward(std::vector<int>& tab, int64_t nz) {
     return true;
 }
 
+// Reorder a packed table's generations into XCD patches (packed_schedule's
+// xcd_w, common.hpp).  A generation is a run of entries with the same
+// length and first plane (the tiles' same chunk, dispatched together).
+static void xcd_patch_order(std::vector<int>& tab, int64_t tiles_x, int w) {
+    constexpr int kXcd = 8;
+    const size_t n = tab.size() / 3;
+    for (size_t g0 = 0; g0 < n;) {
+        size_t g1 = g0 + 1;
+        while (g1 < n && tab[3 * g1 + 1] == tab[3 * g0 + 1] && tab[3 * g1 + 2] == tab[3 * g0 + 2]) ++g1;
+        // the generation's tiles in patch order: column strips of w tiles,
+        // row-major inside a strip
+        std::vector<int> t;
+        for (size_t i = g0; i < g1; ++i) t.push_back(tab[3 * i]);
+        std::stable_sort(t.begin(), t.end(), [&](int a, int b) {
+            const int64_t sa = (a % tiles_x) / w, sb = (b % tiles_x) / w;
+            return sa != sb ? sa < sb : a < b;
+        });
+        // XCD x takes the next cnt[x] tiles of that order, into its positions
+        std::vector<size_t> pos[kXcd];
+        for (size_t i = g0; i < g1; ++i) pos[i % kXcd].push_back(i);
+        size_t k = 0;
+        for (int x = 0; x < kXcd; ++x)
+            for (size_t i : pos[x]) tab[3 * i] = t[k++];
+        g0 = g1;
+    }
+}
+
 int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
                     hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict,
-                    bool faces_out) {
+                    bool faces_out, int64_t tiles_x, int xcd_w) {
     // Only grids of few tiles: with more than 2 tiles per slot the equal
     // chunks already fill the rounds (2048^2 x 512 fp64: packed 1312 vs 1315
     // Gcell/s), and the search would cost host time at the first launch.
@@ -1103,12 +1133,13 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
     };
     static std::mutex mu;
     // map nodes never move: the verdict's address stays valid for the process
-    static std::map<std::tuple<const void*, int, int64_t, int64_t, int, int, int>, Entry> cache;
+    static std::map<std::tuple<const void*, int, int64_t, int64_t, int, int, int, int>, Entry> cache;
     std::unique_lock<std::mutex> lock(mu);
     // STENCIL_TK_PACK_LC (experiments): chunks of exactly this many planes,
     // used whatever the model says
     const int force_lc = senv_int("STENCIL_TK_PACK_LC", 0);
-    const auto key = std::make_tuple(kern, dev, tiles, nz, K, slots, force_lc);
+    if (tiles_x <= 0) xcd_w = 0;
+    const auto key = std::make_tuple(kern, dev, tiles, nz, K, slots, force_lc, xcd_w);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
         std::vector<int> best_tab;
@@ -1116,6 +1147,7 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
         pack_search(tiles, nz, fill, slots, zc, force_lc, &best_tab, &base, &best);
         hit = cache.try_emplace(key).first;
         if (faces_out && !best_tab.empty() && !faces_outward(best_tab, nz)) best_tab.clear();
+        if (xcd_w > 0 && !best_tab.empty()) xcd_patch_order(best_tab, tiles_x, xcd_w);
         if (!best_tab.empty() && (best * 50 < base * 49 || force_lc > 0)) {
             hit->second.workgroups = int64_t(best_tab.size() / 3);
             hit->second.host = std::move(best_tab);
@@ -1360,6 +1392,24 @@ int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots
     if (equal_steps) *equal_steps = base;
     if (packed_steps) *packed_steps = best;
     if (workgroups) *workgroups = (!tab.empty() && best * 50 < base * 49) ? int64_t(tab.size() / 3) : 0;
+    clear_error();
+    return STENCIL_OK;
+}
+int stencil_pack_table(int64_t tiles, int64_t tiles_x, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,
+                       int32_t xcd_width, int32_t* table, int64_t capacity, int64_t* workgroups) {
+    using namespace stencil;
+    if (tiles <= 0 || tiles_x <= 0 || planes <= 0 || fill < 0 || slots <= 0 || zchunk <= 0 || xcd_width < 0 ||
+        planes > (int64_t(1) << 30) || tiles * ((planes + zchunk - 1) / zchunk) > (int64_t(1) << 26))
+        return set_error(STENCIL_EINVAL, "pack table: tiles, tiles_x, planes, slots, zchunk > 0, fill, xcd_width >= 0");
+    std::vector<int> tab;
+    int64_t base = 0, best = 0;
+    pack_search(tiles, planes, fill, slots, zchunk, 0, &tab, &base, &best);
+    if (tab.empty() || best * 50 >= base * 49) tab.clear();
+    if (xcd_width > 0 && !tab.empty()) xcd_patch_order(tab, tiles_x, xcd_width);
+    const int64_t n = int64_t(tab.size() / 3);
+    if (table)
+        for (int64_t i = 0; i < std::min(n, capacity) * 3; ++i) table[i] = tab[size_t(i)];
+    if (workgroups) *workgroups = n;
     clear_error();
     return STENCIL_OK;
 }

@@ -241,10 +241,17 @@ struct HipDev {
     // one-per-CU launch beside them counts on; STENCIL_SLAB_XCU_EXCL=1 also
     // keeps the launches' streams off those CUs.
     static int xcu() { return std::max(0, std::min(16, api_knob("STENCIL_SLAB_XCU", 1))); }
-    static int stream_create(Stream* s, int role, bool confine) {
+    // STENCIL_SLAB_XCU_ALT=c (default 4; 0 = none): the CU budget a staged job
+    // with a confined exchange also tries in its tuning rounds, keeping the
+    // faster (slab_core.hpp staged_tuning_step)
+    static int xcu_alt() {
+        const int a = std::max(0, std::min(16, api_knob("STENCIL_SLAB_XCU_ALT", 4)));
+        return a == xcu() ? 0 : a;
+    }
+    static int stream_create(Stream* s, int role, bool confine, int cus = -1) {
         // STENCIL_SLAB_XCU_EXCL=0 (with a confined exchange): the launches may
-        // use the exchange's CUs too
-        const int c = confine ? xcu() : 0;
+        // use the exchange's CUs too; cus >= 0: that budget instead of xcu()
+        const int c = confine ? (cus >= 0 ? cus : xcu()) : 0;
         const bool excl = c > 0 && api_knob("STENCIL_SLAB_XCU_EXCL", 1) != 0;
         if (role == slab::STREAM_EXCHANGE ? c > 0 : excl) {
             int dev = 0, cus = 0;
@@ -596,6 +603,11 @@ int stencil_slab_round_form(const stencil_slab_job* job, int32_t* form) {
 
 int stencil_slab_round_info(const stencil_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined) {
     return core::round_info<HipDev>(job, form, gated, confined);
+}
+
+int stencil_slab_exchange_budget(const stencil_slab_job* job, int32_t* cus, int32_t* alt_cus, float* round_ms,
+                                 float* alt_round_ms) {
+    return core::exchange_budget<HipDev>(job, cus, alt_cus, round_ms, alt_round_ms);
 }
 
 int stencil_slab_set_timeout(stencil_slab_job* job, int64_t timeout_ms) {

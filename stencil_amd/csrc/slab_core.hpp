@@ -96,7 +96,16 @@ struct Slab {
     // staged rounds: the face span F (0 = the default n / 4 until tuned) and
     // the timing events of the tuning rounds (B on its stream, the exchange)
     int64_t face_span = 0;
-    typename Dev::Event tb0{}, tb1{}, tx0{}, tx1{};
+    typename Dev::Event tb0{}, tb1{}, tx0{}, tx1{}, tr0{};
+    // staged rounds with a confined exchange: the alternative CU budget's
+    // streams (Dev::xcu_alt CUs per XCD for the exchange, the middle launch
+    // off them), swapped in for one timed tuning round and kept where that
+    // round ran faster (staged_tuning_step); xcu = CUs per XCD in use,
+    // round_ms = the tuning rounds' times with the default / alternative
+    typename Dev::Stream sx_alt{}, sb_alt{};
+    int xcu = 0;
+    float round_ms[2] = {0.f, 0.f};
+    float b_ms[2] = {0.f, 0.f}, x_ms[2] = {0.f, 0.f};
     // the grid placement chosen at creation (place_grids): candidates tried
     // and the chosen pair's ms per K-step launch
     int placements = 1;
@@ -130,6 +139,8 @@ struct Job {
     bool confine = false;       // the exchange on a few CUs of its own, the launches off them
     bool staged = false;        // full rounds: face ranges, then the middle beside the exchange
     int tune_left = 2;          // staged: timed rounds left before the face span is set
+    int tune_done = 0;          // staged: timed tuning rounds run (the first: RCCL's connection set-up)
+    int xcu_alt = 0;            // staged + confined: the alternative exchange CU budget tried (0: none)
     bool tuning = false;        // this round records the tuning events
     std::vector<Slab<Dev>> s;
     // kernel timing: events around slab 0's compute launch(es) of every round
@@ -508,6 +519,7 @@ int slab_round_staged(Job<Dev>& j, int k) {
         // received (A waits for X in exchange()'s bracket already)
         if (j.chained) SLAB_TRY(Dev::stream_wait(s.sa, s.ev_int));
         const int64_t F = staged_face_span(j, s);
+        if (j.tuning) SLAB_TRY(Dev::event_record(s.tr0, s.sa));  // the round's start
         SLAB_TRY(time_begin(j, i, s.sa));
         SLAB_TRY(Dev::sweepk(&s.l, src, dst, 0, F, k, s.sa));
         SLAB_TRY(Dev::sweepk(&s.l, src, dst, s.n - F, s.n, k, s.sa));
@@ -814,9 +826,9 @@ void release(JobT* j) {
         if (!drained) continue;
         for (void* p : {s.a, s.b, s.xs, s.xr})
             if (p) Dev::free(p);
-        for (typename Dev::Stream st : {s.sx, s.sa, s.sb})
+        for (typename Dev::Stream st : {s.sx, s.sa, s.sb, s.sx_alt, s.sb_alt})
             if (st) Dev::stream_destroy(st);
-        for (typename Dev::Event e : {s.ev_bnd, s.ev_int, s.ev_join, s.ev_xin, s.ev_xout, s.tb0, s.tb1, s.tx0, s.tx1})
+        for (typename Dev::Event e : {s.ev_bnd, s.ev_int, s.ev_join, s.ev_xin, s.ev_xout, s.tb0, s.tb1, s.tx0, s.tx1, s.tr0})
             if (e) Dev::event_destroy(e);
         for (typename Dev::Event e : s.ring)
             if (e) Dev::event_destroy(e);
@@ -974,6 +986,7 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
             if (j->confine && Dev::staged_rounds()) {
                 j->staged = true;
                 j->signal = false;
+                j->xcu_alt = Dev::xcu_alt();
             }
             // halo-gated launches where a waiting workgroup can never hold
             // the CU the exchange's kernels need (Dev::halo_gate)
@@ -1034,9 +1047,14 @@ int build_job(const stencil_problem& g, int total, const std::vector<int>& idx, 
             (rc = Dev::event_create(&s.ev_xin, false)) || (rc = Dev::event_create(&s.ev_xout, false)))
             break;
         if (j->staged)
-            for (auto* e : {&s.tb0, &s.tb1, &s.tx0, &s.tx1})
+            for (auto* e : {&s.tb0, &s.tb1, &s.tx0, &s.tx1, &s.tr0})
                 if ((rc = Dev::event_create(e, true))) break;
         if (rc) break;
+        s.xcu = j->confine ? Dev::xcu() : 0;
+        if (j->staged && j->confine && j->xcu_alt > 0 &&
+            ((rc = Dev::stream_create(&s.sb_alt, STREAM_INTERIOR, true, j->xcu_alt)) ||
+             (rc = Dev::stream_create(&s.sx_alt, STREAM_EXCHANGE, true, j->xcu_alt))))
+            break;
         s.ring.assign(size_t(kInflight), typename Dev::Event{});
         for (auto& e : s.ring)
             if ((rc = Dev::event_create(&e, false))) break;
@@ -1305,6 +1323,60 @@ int upload(JobT* job, const void* host, int64_t host_row, int64_t host_rows) {
     return STENCIL_OK;
 }
 
+// After each timed tuning round of a staged job (the streams are idle):
+//   1st round: RCCL's lazy connection set-up -- nothing kept;
+//   2nd round: B, the exchange and the round with the default CU budget.
+//     Where the exchange ran at least 0.8x as long as B and an alternative
+//     budget exists (confined exchanges: Dev::xcu_alt CUs per XCD), the
+//     alternative's streams are swapped in for one more tuning round;
+//     otherwise the face span is set from this round;
+//   3rd round: the same with the alternative; each slab keeps the budget
+//     whose round was faster (the alternative only if 2 % faster) and sets
+//     its face span from that round's B and exchange.
+// The rehearsals' emulated wire decided the 1-CU budget; RCCL's
+// P2P kernels over real xGMI links may need more CUs to fill a link -- this
+// lets the first multi-GPU run measure it instead of assuming it.
+template <class Dev>
+int staged_tuning_step(Job<Dev>& j) {
+    const int step = ++j.tune_done;
+    if (step == 1) return STENCIL_OK;
+    const int m = step == 2 ? 0 : 1;
+    bool slow_exchange = false;
+    for (Slab<Dev>& s : j.s) {
+        SLAB_TRY(Dev::set_device(s.device));
+        float rb = 0.f, rx = 0.f;
+        SLAB_TRY(Dev::event_elapsed(&s.b_ms[m], s.tb0, s.tb1));
+        SLAB_TRY(Dev::event_elapsed(&s.x_ms[m], s.tx0, s.tx1));
+        SLAB_TRY(Dev::event_elapsed(&rb, s.tr0, s.tb1));
+        SLAB_TRY(Dev::event_elapsed(&rx, s.tr0, s.tx1));
+        s.round_ms[m] = std::max(rb, rx);
+        slow_exchange = slow_exchange || s.x_ms[m] >= 0.8f * s.b_ms[m];
+    }
+    if (m == 0 && slow_exchange && j.xcu_alt > 0) {
+        for (Slab<Dev>& s : j.s) {
+            std::swap(s.sx, s.sx_alt);
+            std::swap(s.sb, s.sb_alt);
+            s.xcu = j.xcu_alt;
+        }
+        j.tune_left = 1;  // one more timed round, with the alternative
+        return STENCIL_OK;
+    }
+    for (Slab<Dev>& s : j.s) {
+        int keep = 0;
+        if (m == 1) {
+            keep = s.round_ms[1] < 0.98f * s.round_ms[0] ? 1 : 0;
+            if (!keep) {
+                std::swap(s.sx, s.sx_alt);
+                std::swap(s.sb, s.sb_alt);
+                s.xcu = Dev::xcu();
+            }
+        }
+        s.face_span = tuned_face_span(j, s, s.b_ms[keep], s.x_ms[keep]);
+    }
+    j.tune_left = 0;
+    return STENCIL_OK;
+}
+
 template <class Dev>
 int one_round(Job<Dev>& j, int k, bool full) {
     SLAB_TRY(throttle(j));
@@ -1321,14 +1393,8 @@ int one_round(Job<Dev>& j, int k, bool full) {
         if (j.tuning) {
             j.tuning = false;
             SLAB_TRY(sync_bounded(j));
-            if (--j.tune_left == 0)
-                for (Slab<Dev>& s : j.s) {
-                    SLAB_FAIL(j, Dev::set_device(s.device));
-                    float b_ms = 0.f, x_ms = 0.f;
-                    SLAB_FAIL(j, Dev::event_elapsed(&b_ms, s.tb0, s.tb1));
-                    SLAB_FAIL(j, Dev::event_elapsed(&x_ms, s.tx0, s.tx1));
-                    s.face_span = tuned_face_span(j, s, b_ms, x_ms);
-                }
+            --j.tune_left;
+            SLAB_FAIL(j, staged_tuning_step(j));
         }
     }
     else
@@ -1465,6 +1531,20 @@ int round_info(const JobT* job, int32_t* form, int32_t* gated, int32_t* confined
     if (form) *form = round_form_of(*job);
     if (gated) *gated = job->signal && job->gate ? 1 : 0;
     if (confined) *confined = job->confine ? 1 : 0;
+    return STENCIL_OK;
+}
+
+// The exchange's CU budget of slab 0 (staged, confined jobs): CUs per XCD
+// in use, the alternative tried (0: none), and the tuning rounds' times with
+// the default and with the alternative (0: not run).
+template <class Dev, class JobT>
+int exchange_budget(const JobT* job, int32_t* cus, int32_t* alt_cus, float* round_ms, float* alt_round_ms) {
+    if (!job || job->s.empty()) return set_error(STENCIL_EINVAL, "null job");
+    const Slab<Dev>& s = job->s[0];
+    if (cus) *cus = s.xcu;
+    if (alt_cus) *alt_cus = job->xcu_alt;
+    if (round_ms) *round_ms = s.round_ms[0];
+    if (alt_round_ms) *alt_round_ms = s.round_ms[1];
     return STENCIL_OK;
 }
 

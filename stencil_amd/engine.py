@@ -542,6 +542,16 @@ class SlabJob:
                    "stencil_slab_round_info", lib=self.lib)
         return {"form": int(f.value), "gated": bool(g.value), "confined": bool(c.value)}
 
+    def exchange_budget(self) -> dict:
+        """Staged rounds with a confined exchange: the CUs per XCD the
+        exchange uses, the alternative budget tried in the tuning rounds and
+        both tuning rounds' times (stencil_slab_exchange_budget)."""
+        c, a, r0, r1 = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_float(0.0), ctypes.c_float(0.0)
+        _lib.check(self.lib.stencil_slab_exchange_budget(self.job, ctypes.byref(c), ctypes.byref(a), ctypes.byref(r0),
+                                                         ctypes.byref(r1)), "stencil_slab_exchange_budget", lib=self.lib)
+        return {"cus_per_xcd": int(c.value), "alt_cus_per_xcd": int(a.value), "round_ms": round(float(r0.value), 4),
+                "alt_round_ms": round(float(r1.value), 4)}
+
     def set_timeout(self, ms: int) -> None:
         """The job's deadline for every device wait (stencil_slab_set_timeout):
         past it the job fails with STENCIL_ETIMEOUT and aborts its communicators."""

@@ -198,8 +198,14 @@ int take(void* p, size_t bytes, int peer, Comm* c) {
 
 }  // namespace fake
 
+// a fake stream: synchronous, it only remembers its CU budget (the
+// exchange's CU budget tuning: FAKE_SLAB_WIRE_MS below)
+struct FStream {
+    int cus = 0;
+};
+
 struct FakeDev {
-    using Stream = void*;
+    using Stream = FStream*;
     using Event = fake::Event*;
     using Comm = fake::Comm*;
 
@@ -254,7 +260,24 @@ struct FakeDev {
         const char* v = std::getenv("STENCIL_SLAB_STAGED");
         return !(v && *v && std::atoi(v) == 0);
     }
-    static int wire_delay(Stream, size_t) { return STENCIL_OK; }
+    // FAKE_SLAB_WIRE_MS=t: every exchange first sleeps t / cus ms on an
+    // exchange stream confined to `cus` CUs per XCD (t * cus with
+    // FAKE_SLAB_WIRE_INVERT=1): the tuning rounds then see the alternative
+    // budget faster (or slower) and keep it (or not)
+    static int wire_delay(Stream s, size_t) {
+        const char* v = std::getenv("FAKE_SLAB_WIRE_MS");
+        if (!v || std::atof(v) <= 0) return STENCIL_OK;
+        const int c = std::max(1, s ? s->cus : 1);
+        const char* inv = std::getenv("FAKE_SLAB_WIRE_INVERT");
+        const double ms = (inv && std::atoi(inv)) ? std::atof(v) * c : std::atof(v) / c;
+        std::this_thread::sleep_for(std::chrono::microseconds(int64_t(ms * 1000)));
+        return STENCIL_OK;
+    }
+    static int xcu() { return 1; }
+    static int xcu_alt() {
+        const char* v = std::getenv("STENCIL_SLAB_XCU_ALT");
+        return v && *v ? std::max(0, std::atoi(v)) : 4;
+    }
     static int free_bytes(int64_t* out) {
         *out = fake::g_free;
         return STENCIL_OK;
@@ -282,12 +305,12 @@ struct FakeDev {
     static void release_waits(uint32_t* flag, uint64_t*) {
         if (flag) *flag = 1;
     }
-    static int stream_create(Stream* s, int, bool) {
-        static char dummy;
-        *s = &dummy;
+    static int stream_create(Stream* s, int role, bool confine, int cus = -1) {
+        *s = new FStream;
+        (*s)->cus = confine && role == slab::STREAM_EXCHANGE ? (cus >= 0 ? cus : xcu()) : 0;
         return STENCIL_OK;
     }
-    static void stream_destroy(Stream) {}
+    static void stream_destroy(Stream s) { delete s; }
     static int stream_sync(Stream) { return STENCIL_OK; }
     // synchronous streams: everything has completed when it was issued (a
     // receive that never arrives fails at issue, after the comm's timeout)
@@ -680,6 +703,9 @@ int fake_slab_layout_init(const stencil_problem* p, stencil_layout* out) { retur
 int fake_slab_round_form(const fake_slab_job* job, int32_t* form) { return core::round_form<FakeDev>(job, form); }
 int fake_slab_round_info(const fake_slab_job* job, int32_t* form, int32_t* gated, int32_t* confined) {
     return core::round_info<FakeDev>(job, form, gated, confined);
+}
+int fake_slab_exchange_budget(const fake_slab_job* job, int32_t* cus, int32_t* alt, float* ms, float* alt_ms) {
+    return core::exchange_budget<FakeDev>(job, cus, alt, ms, alt_ms);
 }
 int fake_slab_set_timeout(fake_slab_job* job, int64_t ms) { return core::set_timeout<FakeDev>(job, ms); }
 

@@ -100,3 +100,48 @@ def test_invalid_arguments():
         rc, *_ = plan(*args)
         assert rc != 0
         assert b"pack plan" in lib.stencil_last_error_message()
+
+
+def table(tiles, tiles_x, nz, fill, slots, zc, w):
+    lib = _lib.load()
+    n = ctypes.c_int64(0)
+    assert lib.stencil_pack_table(tiles, tiles_x, nz, fill, slots, zc, w, None, 0, ctypes.byref(n)) == 0
+    buf = (ctypes.c_int32 * (3 * n.value))()
+    assert lib.stencil_pack_table(tiles, tiles_x, nz, fill, slots, zc, w, buf, n.value, ctypes.byref(n)) == 0
+    return [tuple(buf[3 * i:3 * i + 3]) for i in range(n.value)]
+
+
+@pytest.mark.parametrize("w", [2, 3, 5, 10])
+def test_xcd_patch_order_permutes_generations_into_patches(w):
+    """stencil_pack_table with an XCD-patch width: C2's packed
+    grid (10 x 11 tiles of 512 planes, K = 4, 256 slots) keeps every
+    position's chunk length and first plane -- the same makespan -- and only
+    permutes tiles within each generation; the tiles one XCD holds in a
+    generation (workgroup i -> XCD i % 8) then have same-XCD x/y neighbours,
+    where the tile-major table has none."""
+    tx, ty = 10, 11
+    base = table(tx * ty, tx, 512, 8, 256, 256, 0)
+    pat = table(tx * ty, tx, 512, 8, 256, 256, w)
+    assert len(base) == len(pat) == 330
+    assert [(z, n) for _, z, n in base] == [(z, n) for _, z, n in pat]
+    gens = {}
+    for i, (t, z, n) in enumerate(pat):
+        gens.setdefault((z, n), []).append((i, t))
+    assert sorted(t for t, _, _ in base) == sorted(t for t, _, _ in pat)
+
+    def shared_neighbours(tab):
+        xcd = {}
+        for i, (t, z, n) in enumerate(tab):
+            xcd[(t, z, n)] = i % 8
+        pairs = 0
+        for (t, z, n), x in xcd.items():
+            bx, by = t % tx, t // tx
+            for dx, dy in ((1, 0), (0, 1)):
+                if bx + dx < tx and by + dy < ty and xcd.get((t + dx + dy * tx, z, n)) == x:
+                    pairs += 1
+        return pairs
+
+    for key, ent in gens.items():
+        assert len({t for _, t in ent}) == len(ent)  # a permutation: every tile once per generation
+    assert shared_neighbours(base) == 0
+    assert shared_neighbours(pat) >= 100 if w > 2 else shared_neighbours(pat) >= 60

@@ -599,3 +599,69 @@ def test_gated_rounds_number_their_exchanges(fake, monkeypatch, nslabs, exchange
         assert_bitwise(job.download(), oracle_grid(spec, nx, ny, nz, k, seed=3))
     finally:
         job.close()
+
+
+@pytest.mark.parametrize("mode", ["one process", "rank mode"])
+@pytest.mark.parametrize("invert,alt_kept", [("0", True), ("1", False)])
+def test_staged_exchange_cu_budget_tuning(fake, monkeypatch, mode, invert, alt_kept):
+    """a staged job with a confined exchange times its
+    exchange with the default CU budget (1 per XCD) and, when the exchange
+    outlasts most of the middle launch, with the alternative (4) in one more
+    tuning round, and keeps the faster.  The fake's exchange stream sleeps
+    FAKE_SLAB_WIRE_MS / cus ms (x cus when inverted), so the alternative is
+    kept, or not; either way the grid stays bitwise one grid, in one process
+    and in rank mode (each rank decides for its own slab)."""
+    monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
+    monkeypatch.setenv("FAKE_SLAB_WIRE_MS", "12")
+    monkeypatch.setenv("FAKE_SLAB_WIRE_INVERT", invert)
+    k = 4
+    fake.set_k(k)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    nx, ny, nz = 10, 6, 12 * 2 + 1
+    sweeps = 5 * k + 2
+
+    def fn(job, r):
+        info = job.round_info()
+        job.fill_initial("random", 4)
+        job.run(sweeps)
+        return info, job.exchange_budget(), job.download()
+
+    if mode == "one process":
+        job = SlabJob(spec, nx, ny, nz, [0, 1], exchange="rccl", lib=fake)
+        try:
+            outs = [fn(job, 0)]
+        finally:
+            job.close()
+    else:
+        outs, errs = _rank_jobs(fake, spec, (nx, ny, nz), 2, fn)
+        assert not any(errs), errs
+    want = oracle_grid(spec, nx, ny, nz, sweeps, seed=4)
+    for info, budget, dense in outs:
+        assert info == {"form": 4, "gated": False, "confined": True}, info
+        assert budget["alt_cus_per_xcd"] == 4 and budget["round_ms"] > 0 and budget["alt_round_ms"] > 0, budget
+        assert budget["cus_per_xcd"] == (4 if alt_kept else 1), budget
+        if alt_kept:
+            assert budget["alt_round_ms"] < budget["round_ms"], budget
+    if mode == "one process":
+        assert_bitwise(outs[0][2], want)
+    else:
+        got = outs[0][2].copy()
+        half = nz // 2 + 1  # rank 0 owns the first 13 planes
+        got[half + 1:] = outs[1][2][half + 1:]
+        assert_bitwise(got, want)
+
+
+def test_staged_exchange_cu_budget_not_tried_for_a_short_exchange(fake, monkeypatch):
+    """An exchange much shorter than the middle launch needs no more CUs: the
+    second tuning round sets the face span and the alternative is never run."""
+    monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
+    fake.set_k(4)
+    spec = StencilSpec(dims=3, dtype="fp64", shape="star")
+    job = SlabJob(spec, 64, 48, 40, [0, 1], exchange="rccl", lib=fake)
+    try:
+        job.fill_initial("random", 4)
+        job.run(6 * 4)
+        b = job.exchange_budget()
+        assert b["cus_per_xcd"] == 1 and b["round_ms"] > 0 and b["alt_round_ms"] == 0, b
+    finally:
+        job.close()

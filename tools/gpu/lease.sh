@@ -45,6 +45,10 @@ for step in "$@"; do
     tests:*) n=$((n + 1))
              timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
              $(echo "${step#tests:}" | tr ',' ' ') > "$O/gpu_tests_part$n.txt" 2>&1 ;;
+    testk:*) IFS=':' read -r tf te <<< "${step#testk:}"   # testk:<file>:<-k expression>
+             n=$((n + 1))
+             timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "$tf" -k "$te" \
+               > "$O/gpu_tests_k$n.txt" 2>&1 ;;
     smoke) timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench.err" ;;
     bench1000) timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline \
@@ -157,6 +161,7 @@ for step in "$@"; do
               wire*) envs+=(STENCIL_SLAB_WIRE_GBPS=${v#wire}) ;;   # emulated xGMI wire time (debug library)
               nox) envs+=(STENCIL_SLAB_XCU=0) ;; noexcl) envs+=(STENCIL_SLAB_XCU_EXCL=0) ;;
               nostage) envs+=(STENCIL_SLAB_STAGED=0) ;; spare*) envs+=(STENCIL_TK_SIG_SPARE=${v#spare}) ;;
+              nogate) envs+=(STENCIL_SLAB_GATE=0) ;; packxcd*) envs+=(STENCIL_TK_PACK_XCD=${v#packxcd}) ;;
               tkxcd*) envs+=(STENCIL_TK_XCD=${v#tkxcd}) ;; noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; place*) envs+=(STENCIL_SLAB_PLACEMENTS=${v#place}) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
               sig*) envs+=(STENCIL_TK_SIG_CHUNKS=${v#sig}) ;; bsig*) envs+=(STENCIL_BOXK_SIG_CHUNKS=${v#bsig}) ;;
               xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
@@ -227,6 +232,26 @@ for step in "$@"; do
           IFS=':' read -r dt nx ny nz sw <<< "${step#sqlib:}"
           PROG=tools/time_lib.py bash profiles/collect_sq.sh "${TAG}_${dt}_${nx}x${ny}x${nz}" \
             stencil_amd/libstencil_hip.so star "$dt" "$nx" "$ny" "$nz" "$sw" 1 > "$O/sq_${dt}_${nx}x${ny}x${nz}.log" 2>&1 ;;
+    abenv:*) # abenv:<dtype>:nx:ny:nz:steps:<V1>;<V2>;.. -- tools/ab.py over variants (each NAME=V[,NAME=V]), interleaved
+          IFS=':' read -r dt nx ny nz st vars <<< "${step#abenv:}"
+          vs=(); IFS=';' read -r -a vl <<< "$vars"; for v in "${vl[@]}"; do vs+=(--variant "$v"); done
+          f="$O/ab_${dt}_${nx}x${ny}x${nz}.txt"; k2=1; while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/ab_${dt}_${nx}x${ny}x${nz}_$k2.txt"; done
+          timeout -k 10 400 python3 tools/ab.py --dtype "$dt" --grid "$nx" "$ny" "$nz" --steps "$st" --reps 7 --launches 10 \
+            "${vs[@]}" > "$f" 2>&1 ;;
+    pmcenv:*) # pmcenv:<dtype>:nx:ny:nz:steps:<NAME=V[,NAME=V]> -- FETCH_SIZE / WRITE_SIZE passes of tools/ab.py's launches
+          IFS=':' read -r dt nx ny nz st ev <<< "${step#pmcenv:}"
+          tg="${dt}_${nx}x${ny}x${nz}_${ev//[=,]/_}"
+          for ctr in FETCH_SIZE WRITE_SIZE; do
+            (cd /tmp && TMPDIR=/tmp timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctr --output-format csv \
+               -d "$O/pmc_${tg}_$ctr" -o run -- python3 "$R/tools/ab.py" --dtype "$dt" --grid "$nx" "$ny" "$nz" \
+               --steps "$st" --reps 1 --launches 5 --variant "$ev" > "$O/pmc_${tg}_$ctr.log" 2>&1) || exit 1
+          done ;;
+    envbench1000:*) # envbench1000:<NAME=V[,NAME=V]> -- the 1000-step C2 bench with those variables (debug library)
+          ev=${step#envbench1000:}
+          f="$O/envbench1000_${ev//[=,]/_}.json"; k2=1
+          while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/envbench1000_${ev//[=,]/_}_$k2.json"; done
+          env ${ev//,/ } timeout -k 10 300 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline --allow-debug-library \
+            > "$f" 2>> "$O/bench.err" ;;
     tierbench) STENCIL_TK_TIER=1 timeout -k 10 200 python3 bench.py --allow-debug-library --steps 1000 --warmup 20 \
              --no-cpu-baseline > "$O/bench_tier.json" 2>> "$O/bench.err" ;;
     *) echo "unknown step $step"; exit 2 ;;
