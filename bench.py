@@ -152,6 +152,9 @@ def parse(argv=None):
                     help="bench even when an experiment knob (a STENCIL_* variable the product ignores) is set, "
                          "i.e. on libstencil_hip_debug.so; the JSON line names the library and the knobs either way")
     args = ap.parse_args(argv)
+    # slab jobs (the C-ABI) search grid placements only when asked (STENCIL_SLAB_PLACEMENTS, default 1):
+    # the bench opts in with its own --placements, as its single-grid engine does (JacobiEngine.place)
+    os.environ.setdefault("STENCIL_SLAB_PLACEMENTS", str(max(1, args.placements)))
     from stencil_amd import _lib
     if _lib.debug_knobs_requested() and not args.allow_debug_library:
         knobs = sorted(k for k in os.environ if k.startswith("STENCIL_") and k not in _lib.API_KNOBS)
@@ -614,7 +617,7 @@ def rank_job_run(args, world, rank, device, spec, grid, rolling, uid, lib=None, 
         job.kernel_timing(True)
         job.run(extra)
         kt = job.kernel_time()
-        xt = job.exchange_time()
+        xt = dict(job.exchange_time(), round_info=job.round_info(), budget=job.exchange_budget())
         job.kernel_timing(False)
         sweeps += extra
         sums = None if args.no_check else job.plane_sums()[info["first"]:info["first"] + info["planes"]].copy()
@@ -664,11 +667,16 @@ def main_rank_job(args, world, rank, local, lib=None, check_device=None):
         elapsed = float(t.item())
         # every rank's exchange times (its transfers over RCCL, and how much of
         # them ran beside its own launches) for the line
-        xrow = torch.tensor([res["xt"]["transfer_ms"], res["xt"]["beside_ms"], float(res["xt"]["exchanges"])],
-                            dtype=torch.float64)
+        x, ri, b = res["xt"], res["xt"]["round_info"], res["xt"]["budget"]
+        xrow = torch.tensor([x["transfer_ms"], x["beside_ms"], float(x["exchanges"]), float(ri["gated"]),
+                             float(ri["confined"]), float(b["cus_per_xcd"]), float(b["alt_cus_per_xcd"]),
+                             b["round_ms"], b["alt_round_ms"]], dtype=torch.float64)
         xrows = [torch.zeros_like(xrow) for _ in range(world)]
         dist.all_gather(xrows, xrow)
-        xts = [{"transfer_ms": float(r[0]), "beside_ms": float(r[1]), "exchanges": int(r[2])} for r in xrows]
+        xts = [{"transfer_ms": float(r[0]), "beside_ms": float(r[1]), "exchanges": int(r[2]),
+                "round_info": {"form": ri["form"], "gated": bool(r[3]), "confined": bool(r[4])},
+                "budget": {"cus_per_xcd": int(r[5]), "alt_cus_per_xcd": int(r[6]), "round_ms": round(float(r[7]), 4),
+                           "alt_round_ms": round(float(r[8]), 4)}} for r in xrows]
         got = None
         if not args.no_check:
             width = plan["grid"][2] // world + 1
@@ -762,7 +770,7 @@ def main_slab_job(args):
     job.kernel_timing(True)
     job.run(extra)
     kt = job.kernel_time()
-    xt = job.exchange_time()
+    xt = dict(job.exchange_time(), round_info=job.round_info(), budget=job.exchange_budget())
     job.kernel_timing(False)
     sweeps += extra
     sums = job.plane_sums() if not args.no_check else None
@@ -812,9 +820,17 @@ def exchange_summary(xts, who):
     rows = []
     for x in xts:
         n = max(1, x["exchanges"])
-        rows.append({"transfer_ms_per_round": round(x["transfer_ms"] / n, 4),
-                     "beside_launch_frac": round(x["beside_ms"] / x["transfer_ms"], 3) if x["transfer_ms"] > 0 else None,
-                     "rounds": x["exchanges"]})
+        row = {"transfer_ms_per_round": round(x["transfer_ms"] / n, 4),
+               "beside_launch_frac": round(x["beside_ms"] / x["transfer_ms"], 3) if x["transfer_ms"] > 0 else None,
+               "rounds": x["exchanges"]}
+        ri, b = x.get("round_info"), x.get("budget")
+        if ri is not None:
+            # halo-gated: the launches never wait for the exchange stream (stencil_slab_round_info)
+            row["halo_gated"], row["confined"] = ri["gated"], ri["confined"]
+        if b is not None and ri is not None and ri["confined"]:
+            # the exchange's CU budget chosen from the tuning rounds (stencil_slab_exchange_budget)
+            row["cu_budget"] = dict(b, chosen=b["cus_per_xcd"])
+        rows.append(row)
     fracs = [r["beside_launch_frac"] for r in rows if r["beside_launch_frac"] is not None]
     return {"basis": f"hipEvents on {who}'s exchange stream over the timed extra rounds: from the end of the face "
                      "wait (or face launches) to the end of the RCCL send/recv; beside = the part that ran while the "

@@ -71,9 +71,13 @@ int stencil_last_error(void);
  * its exchange confined to c CUs of every XCD and its launches off them;
  * 0 = never confined) and STENCIL_SLAB_XCU_EXCL=0 (the launches may use the
  * exchange's CUs too),
- * STENCIL_SLAB_PLACEMENTS=n (default 16: a two-grid slab tries n placements
- * of its grids at creation and keeps the fastest -- the same launch runs 4-8 %
- * apart depending on the grids' physical pages; 1 = the first allocation),
+ * STENCIL_SLAB_PLACEMENTS=n (default 1 = the first allocation; n > 1: a
+ * two-grid slab tries n placements of its grids at creation and keeps the
+ * fastest -- the same launch runs 4-8 % apart in short bursts depending on
+ * the grids' physical pages, 0.8 % over C2's 1000 sweeps.  Cost at
+ * stencil_slab_create*: up to n candidate grid pairs allocated at once,
+ * within a quarter of the free HBM, and about 6 timed K-step launches per
+ * candidate; bench.py opts in with its --placements, default 16),
  * STENCIL_SLAB_TIMEOUT_MS (a slab job's deadline for any device wait,
  * default 60000: stencil_slab_set_timeout), STENCIL_SLAB_ROLLING_OVERLAP=0
  * (rolling slab rounds exchange after the pass instead of beside it),
@@ -336,7 +340,9 @@ int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots
 /* The packed grid itself (host only): {tile, first plane, planes} per
  * workgroup in dispatch order, for a tile grid `tiles_x` wide; xcd_width > 0
  * reorders every generation of equal chunks into XCD patches of that width
- * (the dispatcher deals workgroup i to XCD i % 8).  Writes at most
+ * (the dispatcher deals workgroup i to XCD i % 8); -1: the width with the most
+ * same-XCD x/y neighbour tiles, as long jobs (>= 256 sweeps per call of
+ * stencil_iterate / stencil_slab_run) launch it.  Writes at most
  * `capacity` triples into `table` (may be NULL) and the count to
  * *workgroups (0: no packed grid). */
 int stencil_pack_table(int64_t tiles, int64_t tiles_x, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,

@@ -79,6 +79,20 @@ struct LaunchInfo {
 };
 extern thread_local LaunchInfo* tl_dry_launch;
 
+// Jobs long enough to run at the package power limit (the C2
+// job's launches slow by ~7 % once the limiter engages, ~20 ms into
+// continuous load) take the energy-saving work orders: the packed z-chunk
+// tables in XCD patches (fewer fabric bytes per cell, slower by ~1 % below
+// the limit, faster at it).  stencil_iterate and stencil_slab_run set the
+// hint for the calling thread when a call covers kSustainedSweeps or more.
+constexpr uint32_t kSustainedSweeps = 256;
+extern thread_local bool tl_sustained;
+struct SustainedScope {
+    bool prev;
+    explicit SustainedScope(bool on) : prev(tl_sustained) { tl_sustained = on; }
+    ~SustainedScope() { tl_sustained = prev; }
+};
+
 // A face-signalled slab launch's geometry (a dry launch: nothing runs):
 // x-y tiles, workgroups and one round's resident slots.  slab.hip confines a
 // job's exchange to a few CUs when the launch beside it takes several rounds

@@ -781,9 +781,12 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         // STENCIL_TK_SIG_SPARE (debug library): CUs per XCD the packed
         // face-signalled schedule leaves to the exchange (default 1)
         const int pslots = SIG ? slots - slots / 32 * senv_int("STENCIL_TK_SIG_SPARE", 1) : slots;
-        // STENCIL_TK_PACK_XCD (debug library): the packed table's generations
-        // in XCD patches this many tiles wide (0: tile-major)
-        const int pack_xcd = senv_int("STENCIL_TK_PACK_XCD", 0);
+        // the packed table's generations in XCD patches for long jobs (the
+        // width with the most same-XCD neighbour tiles; C2: 5 of 10 tiles,
+        // reads 1.81x -> 1.46x compulsory, +1-1.5 % at the power limit, -1.5 %
+        // below it: DESIGN.md §5.1), tile-major otherwise; STENCIL_TK_PACK_XCD
+        // (debug library): that width always (0: tile-major)
+        const int pack_xcd = senv_int("STENCIL_TK_PACK_XCD", tl_sustained ? -1 : 0);
         const int rc = packed_schedule(reinterpret_cast<const void*>(kern), dev, gx * gy, nz, K, 2 * K, pslots, zc, s,
                                        tl_dry_launch != nullptr, &sched, &nb, &verdict, SIG, gx, pack_xcd);
         if (rc != STENCIL_OK) return rc;
@@ -1117,6 +1120,36 @@ static void xcd_patch_order(std::vector<int>& tab, int64_t tiles_x, int w) {
     }
 }
 
+// Same-XCD x/y neighbour pairs of a table (workgroup i -> XCD i % 8, per
+// generation), and the patch width in [2, min(tiles_x, 16)] that maximises
+// them (the smallest on ties; 0 when no width beats tile-major).
+static int64_t same_xcd_pairs(const std::vector<int>& tab, int64_t tiles_x) {
+    constexpr int kXcd = 8;
+    std::map<std::tuple<int, int, int>, int> where;  // (tile, first plane, planes) -> XCD
+    for (size_t i = 0; i < tab.size() / 3; ++i) where[{tab[3 * i], tab[3 * i + 1], tab[3 * i + 2]}] = int(i % kXcd);
+    int64_t pairs = 0;
+    for (const auto& [k, x] : where) {
+        const int t = std::get<0>(k);
+        for (int nb : {t + 1, t + int(tiles_x)}) {
+            if (nb == t + 1 && (t + 1) % tiles_x == 0) continue;
+            auto it = where.find({nb, std::get<1>(k), std::get<2>(k)});
+            pairs += it != where.end() && it->second == x;
+        }
+    }
+    return pairs;
+}
+static int best_patch_width(const std::vector<int>& tab, int64_t tiles_x) {
+    int best_w = 0;
+    int64_t best = same_xcd_pairs(tab, tiles_x);
+    for (int w = 2; w <= std::min<int64_t>(tiles_x, 16); ++w) {
+        std::vector<int> t = tab;
+        xcd_patch_order(t, tiles_x, w);
+        const int64_t p = same_xcd_pairs(t, tiles_x);
+        if (p > best) best = p, best_w = w;
+    }
+    return best_w;
+}
+
 int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K, int fill, int slots, int zc,
                     hipStream_t s, bool dry, const int** sched, int64_t* nb, std::atomic<int>** verdict,
                     bool faces_out, int64_t tiles_x, int xcd_w) {
@@ -1139,6 +1172,7 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
     // used whatever the model says
     const int force_lc = senv_int("STENCIL_TK_PACK_LC", 0);
     if (tiles_x <= 0) xcd_w = 0;
+    int xcd_w_used = xcd_w;  // xcd_w < 0: chosen below (best_patch_width)
     const auto key = std::make_tuple(kern, dev, tiles, nz, K, slots, force_lc, xcd_w);
     auto hit = cache.find(key);
     if (hit == cache.end()) {
@@ -1147,14 +1181,15 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
         pack_search(tiles, nz, fill, slots, zc, force_lc, &best_tab, &base, &best);
         hit = cache.try_emplace(key).first;
         if (faces_out && !best_tab.empty() && !faces_outward(best_tab, nz)) best_tab.clear();
-        if (xcd_w > 0 && !best_tab.empty()) xcd_patch_order(best_tab, tiles_x, xcd_w);
+        if (xcd_w < 0 && !best_tab.empty()) xcd_w_used = best_patch_width(best_tab, tiles_x);
+        if (xcd_w_used > 0 && !best_tab.empty()) xcd_patch_order(best_tab, tiles_x, xcd_w_used);
         if (!best_tab.empty() && (best * 50 < base * 49 || force_lc > 0)) {
             hit->second.workgroups = int64_t(best_tab.size() / 3);
             hit->second.host = std::move(best_tab);
         }
         if (senv_int("STENCIL_TK_VERBOSE", 0))
-            std::fprintf(stderr, "pack: equal chunks %lld steps, packed %lld steps (%lld workgroups)%s\n",
-                         (long long)base, (long long)best, (long long)hit->second.workgroups,
+            std::fprintf(stderr, "pack: equal chunks %lld steps, packed %lld steps (%lld workgroups, XCD patches %d wide)%s\n",
+                         (long long)base, (long long)best, (long long)hit->second.workgroups, xcd_w_used,
                          hit->second.host.empty() ? " -- not used" : "");
     }
     Entry& e = hit->second;
@@ -1398,13 +1433,14 @@ int stencil_pack_plan(int64_t tiles, int64_t planes, int32_t fill, int32_t slots
 int stencil_pack_table(int64_t tiles, int64_t tiles_x, int64_t planes, int32_t fill, int32_t slots, int32_t zchunk,
                        int32_t xcd_width, int32_t* table, int64_t capacity, int64_t* workgroups) {
     using namespace stencil;
-    if (tiles <= 0 || tiles_x <= 0 || planes <= 0 || fill < 0 || slots <= 0 || zchunk <= 0 || xcd_width < 0 ||
+    if (tiles <= 0 || tiles_x <= 0 || planes <= 0 || fill < 0 || slots <= 0 || zchunk <= 0 || xcd_width < -1 ||
         planes > (int64_t(1) << 30) || tiles * ((planes + zchunk - 1) / zchunk) > (int64_t(1) << 26))
         return set_error(STENCIL_EINVAL, "pack table: tiles, tiles_x, planes, slots, zchunk > 0, fill, xcd_width >= 0");
     std::vector<int> tab;
     int64_t base = 0, best = 0;
     pack_search(tiles, planes, fill, slots, zchunk, 0, &tab, &base, &best);
     if (tab.empty() || best * 50 >= base * 49) tab.clear();
+    if (xcd_width < 0 && !tab.empty()) xcd_width = best_patch_width(tab, tiles_x);
     if (xcd_width > 0 && !tab.empty()) xcd_patch_order(tab, tiles_x, xcd_width);
     const int64_t n = int64_t(tab.size() / 3);
     if (table)

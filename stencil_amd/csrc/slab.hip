@@ -158,8 +158,10 @@ struct HipDev {
     // exchange confined) instead of staged ones
     static bool staged_rounds() { return api_knob("STENCIL_SLAB_STAGED", 1) != 0; }
     // STENCIL_SLAB_PLACEMENTS=n: grid placements a two-grid slab tries at
-    // creation (default 16; 1 = the first allocation)
-    static int placement_trials() { return std::max(1, api_knob("STENCIL_SLAB_PLACEMENTS", 16)); }
+    // creation (default 1 = the first allocation since round 6: the search
+    // gained 0.8 % at C2's 1000 sweeps, profiles/r06/r06d_bench_1000_place*;
+    // bench.py opts in with its --placements)
+    static int placement_trials() { return std::max(1, api_knob("STENCIL_SLAB_PLACEMENTS", 1)); }
     static bool placement_verbose() { return knob("STENCIL_SLAB_PLACE_VERBOSE", 0) != 0; }
     // STENCIL_SLAB_ROLLING_OVERLAP=0: rolling rounds exchange after the pass
     // (slab_round_rolling) instead of beside it (slab_round_rolling_overlap)
@@ -573,6 +575,7 @@ int stencil_slab_upload(stencil_slab_job* job, const void* host, int64_t host_ro
 }
 
 int stencil_slab_run(stencil_slab_job* job, uint32_t iterations, float* elapsed_ms) {
+    const stencil::SustainedScope sustained(iterations >= stencil::kSustainedSweeps);
     return core::run<HipDev>(job, iterations, elapsed_ms);
 }
 

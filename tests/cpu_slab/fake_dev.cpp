@@ -250,9 +250,12 @@ struct FakeDev {
         const char* v = std::getenv("FAKE_SLAB_CONFINE");
         return v && std::atoi(v) != 0;
     }
-    // FAKE_SLAB_PLACE=n: the placement search's allocation and choice logic (timings are the host's)
+    // the placement search's allocation and choice logic (timings are the
+    // host's): STENCIL_SLAB_PLACEMENTS as the product reads it (default 1),
+    // or FAKE_SLAB_PLACE=n
     static int placement_trials() {
         const char* v = std::getenv("FAKE_SLAB_PLACE");
+        if (!v || !*v) v = std::getenv("STENCIL_SLAB_PLACEMENTS");
         return v && std::atoi(v) > 1 ? std::atoi(v) : 1;
     }
     static bool placement_verbose() { return false; }

@@ -145,3 +145,10 @@ def test_xcd_patch_order_permutes_generations_into_patches(w):
         assert len({t for _, t in ent}) == len(ent)  # a permutation: every tile once per generation
     assert shared_neighbours(base) == 0
     assert shared_neighbours(pat) >= 100 if w > 2 else shared_neighbours(pat) >= 60
+
+
+def test_auto_patch_width_for_c2():
+    """xcd_width = -1 (what long jobs launch): the width with the most same-XCD
+    neighbour tiles -- 5 for C2's 10 x 11 tiles (451 of 597 pairs)."""
+    tx, ty = 10, 11
+    assert table(tx * ty, tx, 512, 8, 256, 256, -1) == table(tx * ty, tx, 512, 8, 256, 256, 5)

@@ -162,6 +162,7 @@ for step in "$@"; do
               nox) envs+=(STENCIL_SLAB_XCU=0) ;; noexcl) envs+=(STENCIL_SLAB_XCU_EXCL=0) ;;
               nostage) envs+=(STENCIL_SLAB_STAGED=0) ;; spare*) envs+=(STENCIL_TK_SIG_SPARE=${v#spare}) ;;
               nogate) envs+=(STENCIL_SLAB_GATE=0) ;; packxcd*) envs+=(STENCIL_TK_PACK_XCD=${v#packxcd}) ;;
+              long) ;;   # --steps 1000 (below)
               tkxcd*) envs+=(STENCIL_TK_XCD=${v#tkxcd}) ;; noplace) envs+=(STENCIL_SLAB_PLACEMENTS=1) ;; place*) envs+=(STENCIL_SLAB_PLACEMENTS=${v#place}) ;; pverb) envs+=(STENCIL_SLAB_PLACE_VERBOSE=1) ;;
               sig*) envs+=(STENCIL_TK_SIG_CHUNKS=${v#sig}) ;; bsig*) envs+=(STENCIL_BOXK_SIG_CHUNKS=${v#bsig}) ;;
               xcu*x) cc=${v#xcu}; envs+=(STENCIL_SLAB_XCU=${cc%x} STENCIL_SLAB_XCU_EXCL=1) ;;
@@ -170,6 +171,7 @@ for step in "$@"; do
             esac
           done
           case "$c" in C5) a="--steps 16 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
+          [[ "$var" == *long* ]] && a="--steps 1000 --warmup 20"
           [ "$nr" != 0 ] && a="$a --rank-of $nr"
           a="$a --allow-debug-library"
           name="xr_${c}_${nr}_${ex}_${var}${tr:+_$tr}"
@@ -221,6 +223,14 @@ for step in "$@"; do
              -d "$O/sust_pmc" -o run -- python3 "$R/tools/sustained_probe.py" --out "$O/sustained_pmc.json" \
              > "$O/sustained_pmc.log" 2>&1) &&
           timeout -k 10 200 python3 tools/sustained_probe.py --out "$O/sustained_plain.json" > "$O/sustained_plain.log" 2>&1 ;;
+    envdriver:*) ev=${step#envdriver:}   # the driver's command (20 steps) with those variables (debug library)
+          f="$O/envdriver_${ev//[=,]/_}.json"; k2=1
+          while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/envdriver_${ev//[=,]/_}_$k2.json"; done
+          env ${ev//,/ } timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
+            --allow-debug-library > "$f" 2>> "$O/bench.err" ;;
+    sustainedenv:*) ev=${step#sustainedenv:}   # the probe without a profiler, with those variables (debug library)
+          env ${ev//,/ } timeout -k 10 200 python3 tools/sustained_probe.py --out "$O/sustained_plain_${ev//[=,]/_}.json" \
+            > "$O/sustained_plain_${ev//[=,]/_}.log" 2>&1 ;;
     placeab) # bench.py --steps 1000 with 1 and 16 grid placements, alternating, three runs each
           for rep in 1 2 3; do
             for p in 1 16; do
@@ -231,7 +241,7 @@ for step in "$@"; do
     sqlib:*) # sqlib:<dtype>:nx:ny:nz:sweeps -- SQ / LDS / TCC counter passes of AUTO's launches of one shape
           IFS=':' read -r dt nx ny nz sw <<< "${step#sqlib:}"
           PROG=tools/time_lib.py bash profiles/collect_sq.sh "${TAG}_${dt}_${nx}x${ny}x${nz}" \
-            stencil_amd/libstencil_hip.so star "$dt" "$nx" "$ny" "$nz" "$sw" 1 > "$O/sq_${dt}_${nx}x${ny}x${nz}.log" 2>&1 ;;
+            "$R/stencil_amd/libstencil_hip.so" star "$dt" "$nx" "$ny" "$nz" "$sw" 1 > "$O/sq_${dt}_${nx}x${ny}x${nz}.log" 2>&1 ;;
     abenv:*) # abenv:<dtype>:nx:ny:nz:steps:<V1>;<V2>;.. -- tools/ab.py over variants (each NAME=V[,NAME=V]), interleaved
           IFS=':' read -r dt nx ny nz st vars <<< "${step#abenv:}"
           vs=(); IFS=';' read -r -a vl <<< "$vars"; for v in "${vl[@]}"; do vs+=(--variant "$v"); done

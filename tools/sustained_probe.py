@@ -64,6 +64,15 @@ class Telemetry(threading.Thread):
                 self.error = f"{type(e).__name__}: {e}"
                 return
             rec = {"t_ns": t}
+            # the data-fabric and memory clocks (not in gpu_metrics): the
+            # memory-bound kernel's time tracks the memory side, not gfxclk
+            for name in ("DF", "MEM", "SOC"):
+                try:
+                    ci = self.smi.amdsmi_get_clock_info(self.handle, getattr(self.smi.AmdSmiClkType, name))
+                    if isinstance(ci.get("clk"), (int, float)):
+                        rec[f"clk_{name.lower()}"] = ci["clk"]
+                except Exception:  # noqa: BLE001 -- not every clock is readable everywhere
+                    pass
             for k, v in m.items():
                 if any(s in k for s in self.KEYS):
                     sv = self._scalar(v)
