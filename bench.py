@@ -100,6 +100,11 @@ KERNEL_SOURCES = {
 }
 
 
+# stencil_iterate / stencil_slab_run calls of at least this many sweeps take
+# the long-job work orders (common.hpp kSustainedSweeps)
+SUSTAINED_SWEEPS = 256
+
+
 def kernel_source_sha(kname: str):
     import hashlib
     h = hashlib.sha256()
@@ -501,6 +506,13 @@ def main_single(args):
         parallelism = "1 GPU, one process, the whole grid (no decomposition)"
         timing = "hipEvents of stencil_iterate over the timed region"
         key = f"3d7pt_fp64_{args.n}cube_per_gpu" if args.config == "C2" else f"{args.config}_slab_{gnz}"
+        # calls of >= 256 sweeps run at the package power limit and take the XCD-patch packed tables
+        # (DESIGN.md §5.2, §6): a separate PMC traffic entry
+        long_job = args.steps >= SUSTAINED_SWEEPS
+        extra["work_order"] = ("XCD-patch packed z-chunk tables (one stencil_iterate call of >= %d sweeps)" if long_job
+                               else "tile-major packed z-chunk tables (a call of < %d sweeps)") % SUSTAINED_SWEEPS
+        if long_job:
+            key += "_long"
         del eng
     # device time per `sweeps_per_launch` sweeps, charged pro rata (with K = 4
     # a 1000-step job is 250 fused launches; a K that does not divide the step

@@ -50,9 +50,10 @@ for step in "$@"; do
              timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "$tf" -k "$te" \
                > "$O/gpu_tests_k$n.txt" 2>&1 ;;
     smoke) timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
-    bench) timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench.err" ;;
-    bench1000) timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline \
-             > "$O/bench_1000.json" 2>> "$O/bench.err" ;;
+    bench) f="$O/bench_driver.json"; k2=1; while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/bench_driver_$k2.json"; done
+           timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$f" 2>> "$O/bench.err" ;;
+    bench1000) f="$O/bench_1000.json"; k2=1; while [ -e "$f" ]; do k2=$((k2 + 1)); f="$O/bench_1000_$k2.json"; done
+             timeout -k 10 200 python3 bench.py --steps 1000 --warmup 20 --no-cpu-baseline > "$f" 2>> "$O/bench.err" ;;
     bench:*) c=${step#bench:}
              case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 32 --warmup 4";; *) a="--steps 40 --warmup 4";; esac
              timeout -k 10 400 python3 bench.py --config "$c" $a > "$O/bench_$c.json" 2>> "$O/bench.err" ;;
@@ -63,6 +64,9 @@ for step in "$@"; do
     prof:*) c=${step#prof:}
             case "$c" in C5) a="--steps 8 --warmup 0";; *) a="--steps 100 --warmup 5";; esac
             bash profiles/collect.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/collect_$c.log" 2>&1 ;;
+    proflong:*) c=${step#proflong:}   # the same at 1000 sweeps (one call: the long-job work orders)
+            bash profiles/collect.sh "${TAG}_${c}long" --config "$c" --steps 1000 --warmup 20 --no-cpu-baseline \
+              > "$O/collect_${c}long.log" 2>&1 ;;
     sq:*) c=${step#sq:}
           case "$c" in C1) a="--steps 100 --warmup 10";; C5) a="--steps 8 --warmup 0";; *) a="--steps 40 --warmup 4";; esac
           PROG=bench.py bash profiles/collect_sq.sh "${TAG}_$c" --config "$c" $a --no-cpu-baseline > "$O/sq_$c.log" 2>&1 ;;
