@@ -55,6 +55,16 @@
 #ifndef TK_PACK2
 #define TK_PACK2 1
 #endif
+// TK_SEG_FAST: a segment (tile, z-chunk) whose region lies inside the grid
+// in x and y and whose stage planes that reach the output lie inside in z
+// runs an instantiation of the plane loop with no ghost-cell selects at all;
+// the choice is made once per segment, so the two loops never share live
+// registers (the per-step choice, kFast, duplicates the step inside the loop).
+// fp64 shapes of the default build (wide-plane grids, slab launches):
+// 2048^2 x 512 +1 % in one process (profiles/r06/r06i_*)
+#ifndef TK_SEG_FAST
+#define TK_SEG_FAST 1
+#endif
 
 namespace stencil {
 namespace {
@@ -78,6 +88,10 @@ __device__ __forceinline__ double sdpp(double v) {
                                                  __builtin_amdgcn_mov_dpp(b.y, CTRL, 0xf, 0xf, true)));
 }
 constexpr int kSShr1 = 0x138, kSShl1 = 0x130;  // wave_shr:1 / wave_shl:1
+// the kernel's `fast` bits (STENCIL_TK_FAST, debug library): kFastStep = the
+// per-step choice (kFast shapes), kFastSeg = the per-segment choice
+// (TK_SEG_FAST), kFastAll = every tile taken as inside (timing only: wrong ghost cells)
+constexpr int kFastStep = 1, kFastAll = 2, kFastSeg = 4;
 
 // The plane loop unrolled N steps (compile-time step index), and the tail of
 // fewer than N steps.
@@ -306,8 +320,31 @@ __global__ void __launch_bounds__(64 * NW)
     // neighbour strips (the first / last wave reads its own: those rows are ring rows)
     const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
 
-    auto segment = [&](auto REV_, auto PROD_) {  // one segment: tile t, planes [za, zb)
+    // the tile's whole region inside the grid in x and y (fast & kFastAll: every
+    // tile -- a timing experiment of the edge tiles' select cost, wrong ghost
+    // cells; STENCIL_TK_FAST, debug library)
+    auto region_inner = [&](int bx, int by, int on) -> bool {
+        return (fast & kFastAll) ||
+               (on && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
+                int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny);
+    };
+    // the next segment (units [lo, hi)) needs no ghost-cell select: its region
+    // is inside in x and y, and for every intermediate stage s the planes
+    // whose t_s reaches the output -- [za - (K - s), zb + K - s) -- are inside
+    // in z (a halo side: the slab's halo planes count as inside).  The planes
+    // the pipeline's fill and drain compute beyond them are never read.
+    auto seg_fast = [&]() -> bool {
+        if (!(fast & kFastSeg)) return false;
+        const int t = int(lo / nzr);
+        const int za = zbeg + int(lo - int64_t(t) * nzr);
+        const int zb = za + (hi - lo < int64_t(zend - za) ? int(hi - lo) : zend - za);
+        if (!region_inner(t % tiles_x, t / tiles_x, 1)) return false;
+        // strongest at s = 1 (the widest reach): [za - K + 1, zb + K - 1)
+        return za - (K - 1) >= (halo_lo ? -(K - 1) : 0) && zb + K - 1 <= (halo_hi ? nz + K - 1 : nz);
+    };
+    auto segment = [&](auto REV_, auto PROD_, auto SFAST_) {  // one segment: tile t, planes [za, zb)
     constexpr bool REV = decltype(REV_)::value;
+    constexpr bool SFAST = decltype(SFAST_)::value;  // the whole segment without ghost-cell selects
     constexpr bool PROD = TIER && decltype(PROD_)::value;  // TIER producer (stores t_K into the slots)
     constexpr bool CONS = TIER && !PROD;                   // TIER consumer (reads the slots)
     const int t = int(lo / nzr);
@@ -362,10 +399,7 @@ __global__ void __launch_bounds__(64 * NW)
     uint32_t tier_pv = 0;  // the prefetched flag
     // the whole region inside the grid in x and y: intermediate stages need no
     // ghost-cell select on steps whose stage planes are all inside in z
-    // (fast == 2: every tile takes the fast path -- a timing experiment of the
-    // edge tiles' select cost, wrong ghost cells; STENCIL_TK_FAST=2, debug library)
-    const bool xy_inner = fast == 2 || (fast && int64_t(bx) * TX - XR * V >= 0 && int64_t(bx) * TX - XR * V + RW <= g.nx &&
-                                        int64_t(by) * TY - K >= 0 && int64_t(by) * TY - K + RH <= g.ny);
+    const bool xy_inner = region_inner(bx, by, fast & kFastStep);
     const int ld_lo = halo_lo ? -K : -1;
     const int ld_hi = halo_hi ? nz + K - 1 : nz;
     const int zfirst = za - K > ld_lo ? za - K : ld_lo;
@@ -633,6 +667,10 @@ __global__ void __launch_bounds__(64 * NW)
         if constexpr (DIAG != 1) load_plane(vin[(S + NS - 2) % NS], p + NS - 2);  // slot of in(p-2), consumed above
     };
     auto step = [&](auto S_, int p) {
+        if constexpr (SFAST) {
+            stepb(S_, p, std::true_type{});
+            return;
+        }
         // compiled for the fp64 one-cell-per-lane shapes only: duplicating the
         // step costs the fp32 / signalled shapes their register fit
         constexpr bool kFast = TK_FAST_PATH && FP && sizeof(T) == 8 && V == 1 && !SIG && DIAG == 0;
@@ -667,15 +705,35 @@ __global__ void __launch_bounds__(64 * NW)
         if (threadIdx.x == 0 && threadIdx.y == 0) tier_publish(tier_mine, tier.base + uint32_t(nz + 1));
     }
     };  // segment
+    // fp64 shapes of the default build only: the fp32 K = 5 strip runs its
+    // select-free loop no faster (4096^2 x 256: 2441 vs 2441 Gcell/s in one
+    // process with 24 % fewer instructions per step), and the
+    // packed-regime fp64 grids (max-ILP build) have the per-step choice
+#ifdef STRIP_ILP_TU
+    constexpr bool kSegFast = false;
+#else
+    constexpr bool kSegFast = TK_SEG_FAST && FP && DIAG == 0 && !TIER && sizeof(T) == 8;
+#endif
+    using F = std::false_type;
+    using Tr = std::true_type;
     while (lo < hi) {
         if constexpr (TIER) {
-            if (tprod) segment(std::false_type{}, std::true_type{});
-            else segment(std::false_type{}, std::false_type{});
+            if (tprod) segment(F{}, Tr{}, F{});
+            else segment(F{}, F{}, F{});
+        } else if constexpr (kSegFast) {
+            const bool sf = seg_fast();
+            if (SIG && rev) {
+                if (sf) segment(Tr{}, F{}, Tr{});
+                else segment(Tr{}, F{}, F{});
+            } else {
+                if (sf) segment(F{}, F{}, Tr{});
+                else segment(F{}, F{}, F{});
+            }
         } else if constexpr (SIG) {
-            if (rev) segment(std::true_type{}, std::false_type{});
-            else segment(std::false_type{}, std::false_type{});
+            if (rev) segment(Tr{}, F{}, F{});
+            else segment(F{}, F{}, F{});
         } else {
-            segment(std::false_type{}, std::false_type{});
+            segment(F{}, F{}, F{});
         }
     }
 }
@@ -794,12 +852,13 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
         if (verdict && verdict->load() == kPackEqual) sched = nullptr, nb = nb_equal, verdict = nullptr;
     }
     if (nb > (int64_t(1) << 31) - 1) return set_error(STENCIL_EINVAL, "grid too large for tkstrip");
-    // interior steps without ghost-cell selects (fp64 one-cell-per-lane shapes):
-    // by default only where the packed schedule runs -- few tiles, 512^3 fp64
-    // 1212 vs 1175 Gcell/s -- since on large planes the duplicated step loses
-    // (2048^2 x 512 1357 vs 1384, 2048^3 1310 vs 1365; profiles/r02o_ab_tk_fast.log)
+    // interior steps without ghost-cell selects, per step (fp64 one-cell-per-lane
+    // shapes): by default only where the packed schedule runs -- few tiles,
+    // 512^3 fp64 1212 vs 1175 Gcell/s -- since on large planes the duplicated
+    // step loses (2048^2 x 512 1357 vs 1384, 2048^3 1310 vs 1365;
+    // profiles/r02o_ab_tk_fast.log); per segment (TK_SEG_FAST) wherever compiled
     const int fast_env = senv_int("STENCIL_TK_FAST", -1);
-    auto fast_of = [&](bool packed) { return fast_env >= 0 ? fast_env : (packed ? 1 : 0); };
+    auto fast_of = [&](bool packed) { return fast_env >= 0 ? fast_env : (packed ? kFastStep : 0) | kFastSeg; };
     if (senv_int("STENCIL_TK_VERBOSE", 0)) {
         int per_cu = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0);
@@ -1384,6 +1443,9 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             case 830708: return launch_st<float, 2, 7, 8, 5, false, 0, false, 4, true, true>(l, in, out, begin, end, s);
             // the default shape from this file's build (AUTO takes the max-ILP build)
             case 20508: return launch_st<float, 2, 5, 8, 5>(l, in, out, begin, end, s);
+            // input planes loaded 3 / 4 planes ahead (NS = 5 / 6) instead of 2
+            case 520508: return launch_st<float, 2, 5, 8, 5, true, 0, false, 5>(l, in, out, begin, end, s);
+            case 620508: return launch_st<float, 2, 5, 8, 5, true, 0, false, 6>(l, in, out, begin, end, s);
             default: return launch_tkstrip_ilp(l, in, out, begin, end, 5, s);
             }
         }

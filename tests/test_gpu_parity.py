@@ -304,22 +304,25 @@ def test_tkstrip_chunking(gpu, monkeypatch, steps, strip, zchunk, dtype, shape3)
         assert same_bits(got, want), it
 
 
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
 @pytest.mark.parametrize("steps", ["3", "4", "5"])
-@pytest.mark.parametrize("fast", ["0", "1"])
+@pytest.mark.parametrize("fast", ["0", "1", "4", "5"])
 @pytest.mark.parametrize("zchunk", ["0", "5", "11"])
-def test_tkstrip_interior_fast_path(gpu, monkeypatch, steps, fast, zchunk):
-    """fp64 one-cell-per-lane strip shapes skip the intermediate stages'
-    ghost-cell select on steps where the region lies inside the grid in x, y
-    and every stage plane in z (STENCIL_TK_FAST): interior and edge tiles,
-    z-chunk seams and the z ends, bitwise equal to the oracle either way."""
+def test_tkstrip_interior_fast_path(gpu, monkeypatch, dtype, steps, fast, zchunk):
+    """The strip kernel skips the intermediate stages' ghost-cell select
+    where the region lies inside the grid in x and y and the stage planes in
+    z (STENCIL_TK_FAST bits): per step (1, fp64 one-cell-per-lane shapes) or
+    per segment (4, every shape: a tile's z-chunk whose reach stays off the z
+    ends).  Interior and edge tiles, z-chunk seams and the z ends, bitwise
+    equal to the oracle whichever way."""
     monkeypatch.setenv("STENCIL_TK_STEPS", steps)
     monkeypatch.setenv("STENCIL_TK_ZCHUNK", zchunk)
     monkeypatch.setenv("STENCIL_TK_FAST", fast)
     nx, ny, nz = 300, 250, 40
-    p = ob.problem(3, "fp64", "star", 1, "naive", nx, ny, nz)
+    p = ob.problem(3, dtype, "star", 1, "naive", nx, ny, nz)
     for it in (int(steps), 2 * int(steps) + 1):
         want = ob.run(p, it, "random", 41 + it)
-        _, got = gpu_run(gpu, 3, "fp64", "star", 1, "naive", "temporalk", nx, ny, nz, it, "random", 41 + it)
+        _, got = gpu_run(gpu, 3, dtype, "star", 1, "naive", "temporalk", nx, ny, nz, it, "random", 41 + it)
         assert same_bits(got, want), it
 
 
