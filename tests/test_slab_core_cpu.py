@@ -619,7 +619,9 @@ def test_staged_exchange_cu_budget_tuning(fake, monkeypatch, mode, invert, alt_k
     kept, or not; either way the grid stays bitwise one grid, in one process
     and in rank mode (each rank decides for its own slab)."""
     monkeypatch.setenv("FAKE_SLAB_CONFINE", "1")
-    monkeypatch.setenv("FAKE_SLAB_WIRE_MS", "12")
+    # 40 ms (10 ms with the alternative): a margin no scheduling hiccup of a
+    # loaded host (pytest -n, the fake's threads) closes
+    monkeypatch.setenv("FAKE_SLAB_WIRE_MS", "40")
     monkeypatch.setenv("FAKE_SLAB_WIRE_INVERT", invert)
     k = 4
     fake.set_k(k)
