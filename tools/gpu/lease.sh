@@ -19,6 +19,7 @@
 #   fastab           tools/ab.py at 512^3: the interior fast path as shipped vs on every tile (timing only) vs off
 #   libab:<t1,t2..>  (LIBAB_FP32_ONLY=1: fp32 shapes only) tools/time_lib.py on build/variants/lib_<t>.so (tools/lib_variants.sh), one process per run,
 #                    alternating the variants, 3 rounds over C2 / 2048^2 x 512 / NS / fp32 4096^2 x 256
+#   libdigest:<t,..> tools/lib_digest.py per variant and the product library (bitwise check of variants)
 #   libabbox:<t,..>  the same over box shapes: C5 2048^3 / 2048^2 x 256 / 512^3 fp64
 #   rankof:<cfg>:<N>[:nosig] bench.py --config <cfg> --rank-of N --exchange loopback: one interior rank of the N-GPU job
 #   plain:<star|box>:<dt>:nx:ny:nz:sweeps  tools/time_lib.py on the product library (one grid, AUTO)
@@ -95,6 +96,18 @@ for step in "$@"; do
                  done
                done
              done ;;
+    libdigest:*) # libdigest:<t1,t2..> -- tools/lib_digest.py per variant (and the product library): equal digests per
+          # shape = bitwise equal results; odd nx (partial fp32 lane pairs), big / small planes, fp32 and fp64
+          IFS=',' read -r -a tags <<< "${step#libdigest:}"
+          for shp in "star fp32 4096 4096 64 23" "star fp32 1031 517 40 13" "star fp32 300 250 40 7" \
+                     "star fp32 2049 1023 96 11" "star fp64 512 512 512 9" "star fp64 2048 2048 64 9" "star fp64 301 257 33 6"; do
+            for t in product "${tags[@]}"; do
+              lib="build/variants/lib_$t.so"; [ "$t" = product ] && lib=stencil_amd/libstencil_hip.so
+              # shellcheck disable=SC2086
+              timeout -k 10 120 python3 tools/lib_digest.py "$lib" $shp | sed "s/^/$t: /" >> "$O/lib_digest.txt" \
+                2>> "$O/lib_ab.err" || exit 1
+            done
+          done ;;
     libabbox:*) IFS=',' read -r -a tags <<< "${step#libabbox:}"
              for rep in 1 2 3; do
                for shp in "box fp64 2048 2048 2048 16 2" "box fp64 2048 2048 256 40 2" "box fp64 512 512 512 200 2"; do
