@@ -30,7 +30,7 @@ SRCS := $(wildcard stencil_amd/csrc/*.hip)
 OBJ ?= build/obj
 # kernels_boxk_probe.hip (a code-generation probe) is built twice, with and without SLP
 # vectorisation, and linked into the debug library only; the product links knobs.cpp's stubs instead
-PROBE_OBJS := $(OBJ)/kernels_boxk_probe.o $(OBJ)/kernels_boxk_probe_noslp.o
+PROBE_OBJS := $(OBJ)/kernels_boxk_probe.o $(OBJ)/kernels_boxk_probe_noslp.o $(OBJ)/kernels_strip_probe.o
 OBJS := $(filter-out $(PROBE_OBJS),$(patsubst stencil_amd/csrc/%.hip,$(OBJ)/%.o,$(SRCS)))
 HOST_SRCS := $(wildcard stencil_amd/csrc/host/*.cpp)
 HOST_HDRS := $(wildcard stencil_amd/csrc/host/*.hpp)
@@ -56,6 +56,9 @@ $(OBJ)/knobs_debug.o: stencil_amd/csrc/knobs.cpp stencil_amd/csrc/common.hpp inc
 # flag goes to the device compilation only (the host x86 backend has no such scheduler)
 $(OBJ)/kernels_strip_ilp.o: stencil_amd/csrc/kernels_strip.hip
 $(OBJ)/kernels_strip_ilp.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-ilp
+# the strip probe (debug library only): the max-ILP shapes again, as a compile-time variant
+$(OBJ)/kernels_strip_probe.o: stencil_amd/csrc/kernels_strip.hip
+$(OBJ)/kernels_strip_probe.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-ilp
 # the 2D kernels (tb2ds / tb2d / tb2d1) under the same scheduler: C1 fp64 +1.4 %, fp32 +2.3 %, the rest within
 # +-1.3 % (profiles/r03/r03am_*, r03an_*)
 $(OBJ)/kernels_tb2d.o: HIPFLAGS += -Xarch_device -mllvm=-misched=gcn-max-ilp

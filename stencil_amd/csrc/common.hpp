@@ -188,6 +188,10 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
 // machine scheduler (launch_tkstrip routes the shapes measured faster that way)
 int launch_tkstrip_ilp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                        hipStream_t s);
+// kernels_strip_probe.hip (debug library only; the product links knobs.cpp's stub): the max-ILP shapes
+// built as a compile-time variant, debug cfg 97
+int launch_tkstrip_probe(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                         hipStream_t s);
 // The halo gate of a face-signalled launch (stencil_sweepk_signal_gated):
 // the workgroups whose z range reaches a halo plane first wait until *word
 // (the slab's exchange-completion word, stencil_exchange_done) has reached

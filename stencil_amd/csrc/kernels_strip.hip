@@ -65,21 +65,10 @@
 #ifndef TK_SEG_FAST
 #define TK_SEG_FAST 1
 #endif
-// TK_BUF_STORE: the output rows go out as one unconditional raw buffer store
-// per row, the rows / lanes / steps that store nothing given an out-of-range
-// offset (dropped by the hardware), instead of a store behind lane branches.
-// The compiler's waitcnt pass counts a store behind a branch as possibly
-// absent, so the wait for plane p's loads came out as vmcnt(RY-1-k) + RY:
-// it also waited for the previous step's stores, one more per row.  With the
-// stores unconditional the counts include them.
 // TK_ILP_NS32: the input-plane ring of the max-ILP fp32 K = 5 strip (4: loads
 // two planes ahead)
 #ifndef TK_ILP_NS32
 #define TK_ILP_NS32 4
-#endif
-// 1: fp32 shapes, 2: every shape
-#ifndef TK_BUF_STORE
-#define TK_BUF_STORE 0
 #endif
 
 namespace stencil {
@@ -89,20 +78,6 @@ template <typename T, int V>
 struct VecS {
     typedef T type __attribute__((ext_vector_type(V)));
 };
-
-// a nontemporal raw buffer store of one lane's vector (8 or 16 B) at byte
-// offset vo of the resource (TK_BUF_STORE; aux 2 = nt on gfx950)
-template <typename VT>
-__device__ __forceinline__ void buf_store_nt(const VT& v, __amdgpu_buffer_rsrc_t rs, uint32_t vo) {
-    if constexpr (sizeof(VT) == 8) {
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, int(vo), 0, 2);
-    } else {
-        static_assert(sizeof(VT) == 16, "8 or 16 B per lane");
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, int(vo), 0, 2);
-    }
-}
 
 __device__ __forceinline__ float sfma0(float s, float a) { return __builtin_fmaf(s, a, 0.0f); }
 __device__ __forceinline__ double sfma0(double s, double a) { return __builtin_fma(s, a, 0.0); }
@@ -563,16 +538,6 @@ __global__ void __launch_bounds__(64 * NW)
         const int zo = p - K;  // t_K(p-K) -> HBM
         const bool do_store = DIAG != 3 && zo >= za && zo < zb;
         char* obase = dst + int64_t(zr(zo)) * plane * int64_t(sizeof(T));
-        // the plane's store resource: no record at all on a step that stores nothing
-        constexpr bool kBufStore = TK_BUF_STORE && !PROD && (TK_BUF_STORE >= 2 || sizeof(T) == 4);
-        // (uniform values; readfirstlane keeps the resource in SGPRs -- the
-        // divergence analysis cannot see it and would build a waterfall loop)
-        const uint64_t ob = uint64_t(obase);
-        char* const obase_s = reinterpret_cast<char*>(
-            uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(ob))))) |
-            (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(ob >> 32))))) << 32));
-        const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-            obase_s, 0, __builtin_amdgcn_readfirstlane(do_store ? int(0xFFFFFFFFu) : 0), 0x00020000);
 #pragma unroll
         for (int k = 0; k < RY; ++k) {
             VT prev{};  // this row's result of the previous stage
@@ -648,19 +613,7 @@ __global__ void __launch_bounds__(64 * NW)
                                       off[k], prev);
                 continue;
             }
-            if constexpr (kBufStore) {
-                // whole vectors: one store, issued every step and row
-                const uint32_t vo = st[k] && xst[V - 1] ? off[k] : 0xFFFFFFFFu;
-                buf_store_nt(prev, orsrc, vo);
-                if constexpr (V > 1) {  // a lane whose last cell is past nx (odd nx): its cells one by one
-                    if (do_store && st[k] && !xst[V - 1]) {
-                        T* q = reinterpret_cast<T*>(obase + off[k]);
-#pragma unroll
-                        for (int j = 0; j < V - 1; ++j)
-                            if (xst[j]) q[j] = prev[j];
-                    }
-                }
-            } else if (do_store && st[k]) {
+            if (do_store && st[k]) {
                 T* q = reinterpret_cast<T*>(obase + off[k]);
                 if (xst[V - 1]) {
                     __builtin_nontemporal_store(prev, reinterpret_cast<VT*>(q));
@@ -1092,8 +1045,12 @@ int tier_end(TierJob* j, hipStream_t s, bool* failed) {
 // kernels_strip_ilp.hip: the two default shapes measured faster when this file is compiled under LLVM's
 // gcn-max-ilp machine scheduler: the fp64 K = 4 strip on grids of at most 2 tiles per
 // CU slot (the packed schedule with its interior fast path: 512^3 +1.5 %) and the fp32 K = 5 strip (C3).
-int launch_tkstrip_ilp(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
-                       hipStream_t s) {
+// (kernels_strip_probe.hip builds this TU a third time, as launch_tkstrip_probe: a compile-time variant)
+#ifndef STRIP_ILP_FN
+#define STRIP_ILP_FN launch_tkstrip_ilp
+#endif
+int STRIP_ILP_FN(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
+                 hipStream_t s) {
     if (l.prob.dtype == STENCIL_F64 && steps == 4) return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
     if (l.prob.dtype == STENCIL_F32 && steps == 5)
         return launch_st<float, 2, 5, 8, 5, true, 0, false, TK_ILP_NS32>(l, in, out, begin, end, s);
@@ -1426,6 +1383,8 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
                    int cfg, hipStream_t s) {
     if (!temporal2_supports(l.prob))
         return set_error(STENCIL_EUNSUPPORTED, "tkstrip supports the 3D r=1 naive 7-point star only");
+    // debug cfg 97: the max-ILP shapes from kernels_strip_probe.hip (debug library only)
+    if (cfg == 97) return launch_tkstrip_probe(l, in, out, begin, end, steps, s);
     if (l.prob.dtype == STENCIL_F32) {
         if (steps == 3) {
             switch (cfg) {

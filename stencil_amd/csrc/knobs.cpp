@@ -38,6 +38,9 @@ int launch_boxk_probe_slp(const stencil_layout&, const void*, void*, int64_t, in
 int launch_boxk_probe_noslp(const stencil_layout&, const void*, void*, int64_t, int64_t, int, int, hipStream_t) {
     return set_error(STENCIL_EUNSUPPORTED, "the box probe shapes are in libstencil_hip_debug.so only");
 }
+int launch_tkstrip_probe(const stencil_layout&, const void*, void*, int64_t, int64_t, int, hipStream_t) {
+    return set_error(STENCIL_EUNSUPPORTED, "the strip probe shapes are in libstencil_hip_debug.so only");
+}
 #endif
 
 }  // namespace stencil

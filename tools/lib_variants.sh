@@ -11,7 +11,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 IFS=',' read -r -a SRCS <<< "$1"; shift
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -fno-gpu-flush-denormals-to-zero -Wno-pass-failed -Iinclude -Istencil_amd/csrc"
 mkdir -p build/variants
-EXCL=(-e '/knobs_debug.o$' -e '/kernels_boxk_probe')
+EXCL=(-e '/knobs_debug.o$' -e '/kernels_boxk_probe' -e '/kernels_strip_probe')
 for src in "${SRCS[@]}"; do EXCL+=(-e "/$(basename "$src" .hip).o\$"); done
 OTHERS=$(ls build/obj/*.o | grep -v "${EXCL[@]}")
 per_file_flags() {  # the Makefile's per-file device flags
