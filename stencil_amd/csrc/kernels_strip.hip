@@ -70,6 +70,12 @@
 #ifndef TK_ILP_NS32
 #define TK_ILP_NS32 4
 #endif
+// TK_PROBE_NOBAR (kernels_strip_probe.hip only, timing experiment: results
+// wrong): the plain launches' per-step workgroup barrier left out -- the upper
+// bound of what a barrier-free plane step could gain
+#ifndef TK_PROBE_NOBAR
+#define TK_PROBE_NOBAR 0
+#endif
 
 namespace stencil {
 namespace {
@@ -115,16 +121,24 @@ __device__ __forceinline__ void tail_steps(F& f, int p, int plast) {
     }
 }
 
-template <typename T, int V, int RY, int NW, int K, bool DB>
+// SPLIT: each wave holds TWO strips, one per half-wave (lanes 0..31 strip w,
+// lanes 32..63 strip NW + w), so a strip row is 32 lanes x V cells: with V = 4
+// fp32 every plane load / store is a 16-B lane vector (half the memory
+// instructions of the 8-B V = 2 shape for the same region width), while the
+// y-neighbours stay in the lane's registers.  The x lane shifts cross the
+// half boundary (lane 32 reads lane 31) only inside the x ring.
+template <typename T, int V, int RY, int NW, int K, bool DB, bool SPLIT = false>
 struct StripTile {
+    static constexpr int LW = SPLIT ? 32 : 64;       // lanes per strip row
+    static constexpr int NSTR = SPLIT ? 2 * NW : NW; // strips per region
     static constexpr int XR = (K + V - 1) / V;  // ring vectors per x side
-    static constexpr int RW = 64 * V;           // region width
+    static constexpr int RW = LW * V;           // region width
     static constexpr int TX = RW - 2 * XR * V;  // output tile width
-    static constexpr int RH = NW * RY;          // region height
+    static constexpr int RH = NSTR * RY;        // region height
     static constexpr int TY = RH - 2 * K;       // output tile height
     static constexpr int NB = DB ? 2 : 1;       // boundary-row buffers (plane parity)
-    // boundary rows: [buffer][stage input][wave][top, bottom][RW]
-    static constexpr size_t lds_bytes = size_t(NB) * K * NW * 2 * RW * sizeof(T);
+    // boundary rows: [buffer][stage input][strip][top, bottom][RW]
+    static constexpr size_t lds_bytes = size_t(NB) * K * NSTR * 2 * RW * sizeof(T);
 };
 
 // TIER (the two-tier job): a launch of 2 x tiles
@@ -233,19 +247,21 @@ __device__ __forceinline__ void sc1_store(void* p, const VT& v) {
 // for 7 ds_write_b64 + 28 ds_read_b64 per wave and step, which pays for one
 // more fused sweep (K = 5) at the same 7-row strips.
 template <typename T, int V, int RY, int NW, int K, bool DB, int DIAG = 0, bool SIG = false, int NS = 4, bool FP = true,
-          bool HL = false, bool TIER = false>
+          bool HL = false, bool TIER = false, bool SPLIT = false>
 __global__ void __launch_bounds__(64 * NW)
     tkstrip_7pt(const T* __restrict__ in, T* __restrict__ out, Geom g, int zbeg, int zend, int zchunk,
                 int tiles_x, int tiles_y, int halo_lo, int halo_hi, T avg, unsigned* __restrict__ sig,
                 unsigned long long* __restrict__ fsig, const int* __restrict__ sched, int fast, int xcd_pw,
                 TierArgs tier, StripGate gate) {
-    using Tl = StripTile<T, V, RY, NW, K, DB>;
+    using Tl = StripTile<T, V, RY, NW, K, DB, SPLIT>;
     using VT = typename VecS<T, V>::type;
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
+    constexpr int LW = Tl::LW, NSTR = Tl::NSTR;
+    static_assert(!SPLIT || !TIER, "SPLIT: plain or face-signalled launches");
     static_assert(TY > 0 && TX > 0, "tile too small for K");
     static_assert(RY >= 2, "a strip needs a first and a last row");
     static_assert(!HL || K >= 2, "HL keeps stage 1's history");
-    __shared__ __attribute__((aligned(16))) T L[NB][K][NW][2][RW];
+    __shared__ __attribute__((aligned(16))) T L[NB][K][NSTR][2][RW];
     // HL: t_1 history [plane parity][region row][x], each wave its own rows
     __shared__ __attribute__((aligned(16))) T HLs[HL ? 2 : 1][HL ? RH : 1][HL ? RW : 1];
 
@@ -305,6 +321,9 @@ __global__ void __launch_bounds__(64 * NW)
     }
 
     const int lane = threadIdx.x, w = threadIdx.y;
+    // this lane's strip (vw) and its lane within the strip row (hl)
+    const int vw = SPLIT ? (lane >> 5) * NW + w : w;
+    const int hl = SPLIT ? (lane & 31) : lane;
     const int nz = int(g.nz);
     const int64_t plane = g.plane;
     // Addresses are a uniform per-plane base (SGPRs) + a non-negative 32-bit
@@ -321,9 +340,9 @@ __global__ void __launch_bounds__(64 * NW)
         for (int i = threadIdx.y * 64 + threadIdx.x; i < N16; i += 64 * NW) l16[i] = VT{};
     }
 
-    const int xl = lane * V;
+    const int xl = hl * V;
     // neighbour strips (the first / last wave reads its own: those rows are ring rows)
-    const int wa = w > 0 ? w - 1 : 0, wb = w < NW - 1 ? w + 1 : NW - 1;
+    const int wa = vw > 0 ? vw - 1 : 0, wb = vw < NSTR - 1 ? vw + 1 : NSTR - 1;
 
     // the tile's whole region inside the grid in x and y (fast & kFastAll: every
     // tile -- a timing experiment of the edge tiles' select cost, wrong ghost
@@ -358,8 +377,8 @@ __global__ void __launch_bounds__(64 * NW)
     lo += zb - za;
     const int bx = t % tiles_x;
     const int by = t / tiles_x;
-    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(lane) * V;
-    const int64_t y0 = int64_t(by) * TY - K + int64_t(w) * RY;  // this wave's first row
+    const int64_t x = int64_t(bx) * TX - XR * V + int64_t(hl) * V;
+    const int64_t y0 = int64_t(by) * TY - K + int64_t(vw) * RY;  // this strip's first row
 
     // Unconditional loads from clamped addresses (kernels_temporalk.hip): the
     // plane wait is then a counted vmcnt, not vmcnt(0).
@@ -369,12 +388,12 @@ __global__ void __launch_bounds__(64 * NW)
     const int64_t xc = x < xmax ? x : xmax;
 #pragma unroll
     for (int k = 0; k < RY; ++k) {
-        const int rr = w * RY + k;
+        const int rr = vw * RY + k;
         const int64_t y = y0 + k;
         const int64_t yc = y < -1 ? -1 : (y > g.ny ? g.ny : y);
         off[k] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
         yin[k] = y >= 0 && y < g.ny;
-        st[k] = rr >= K && rr < RH - K && y < g.ny && lane >= XR && lane < 64 - XR;
+        st[k] = rr >= K && rr < RH - K && y < g.ny && hl >= XR && hl < LW - XR;
     }
     bool xin[V], xst[V];
 #pragma unroll
@@ -451,11 +470,11 @@ __global__ void __launch_bounds__(64 * NW)
     VT H[K > 1 ? K - 1 : 1][2][RY]; // H[s-1][(q - p0) & 1] holds t_s(q), s < K (HL: s >= 2 only)
     // t_s(q) of parity `par`, row k: stage 1 from LDS with HL, else registers
     auto hget = [&](int s, int par, int k) -> VT {
-        if (HL && s == 1) return *reinterpret_cast<const VT*>(&HLs[par][w * RY + k][xl]);
+        if (HL && s == 1) return *reinterpret_cast<const VT*>(&HLs[par][vw * RY + k][xl]);
         return H[s - 1][par][k];
     };
     auto hset = [&](int s, int par, int k, const VT& v) {
-        if (HL && s == 1) *reinterpret_cast<VT*>(&HLs[par][w * RY + k][xl]) = v;
+        if (HL && s == 1) *reinterpret_cast<VT*>(&HLs[par][vw * RY + k][xl]) = v;
         else H[s - 1][par][k] = v;
     };
 #pragma unroll
@@ -494,8 +513,8 @@ __global__ void __launch_bounds__(64 * NW)
     auto stepb = [&](auto S_, int p, auto FAST_) {
         constexpr int S = decltype(S_)::value;  // (p - p0) % LCM
         constexpr bool FAST = decltype(FAST_)::value;  // no ghost-cell selects this step
-        // fp32 two cells per lane: packed math (-DTK_PACK2=0 builds keep the scalar loop)
-        constexpr bool kPack2 = TK_PACK2 && sizeof(T) == 4 && V == 2;
+        // fp32 two cells per lane (four: SPLIT): packed math (-DTK_PACK2=0 builds keep the scalar loop)
+        constexpr bool kPack2 = TK_PACK2 && sizeof(T) == 4 && (V == 2 || (V == 4 && SPLIT));
         constexpr int P = DB ? (S & 1) : 0;  // buffer written this step
         constexpr int PR = DB ? (P ^ 1) : 0; // buffer read this step
         if constexpr (TIER) {
@@ -511,7 +530,7 @@ __global__ void __launch_bounds__(64 * NW)
                     tier_spin(tier_flags + tnb * kTierFlagStride, tier.base + uint32_t(need), tier.fail);
             }
         }
-        __syncthreads();  // boundary rows of step p-1 are visible
+        if constexpr (!(TK_PROBE_NOBAR && !SIG && !TIER)) __syncthreads();  // boundary rows of step p-1 are visible
         if constexpr (TIER) {
             // every wave's wait above is behind the barrier: publish the planes
             // stored (producer: t_K up to p-K-1) / loaded (consumer: up to p)
@@ -567,12 +586,14 @@ __global__ void __launch_bounds__(64 * NW)
                     // the rest in packed math (v_pk_add_f32 / v_pk_fma_f32:
                     // both cells of the lane per instruction, each
                     // IEEE-rounded as the scalar op)
-                    VT sum = VT{wl + c[1], c[0] + er};
+                    VT sum;
+                    if constexpr (V == 2) sum = VT{wl + c[1], c[0] + er};
+                    else sum = VT{wl + c[1], c[0] + c[2], c[1] + c[3], c[2] + er};
                     sum += up;
                     sum += dn;
                     sum += REV ? zp : zm;
                     sum += REV ? zm : zp;
-                    o = DIAG == 2 ? c : __builtin_elementwise_fma(sum, VT{avg, avg}, VT{});
+                    o = DIAG == 2 ? c : __builtin_elementwise_fma(sum, (VT)(avg), VT{});
 #pragma unroll
                     for (int j = 0; j < V; ++j) {
                         if (s < K && !FAST) o[j] = (zin[s - 1] && yin[k] && xin[j]) ? o[j] : c[j];
@@ -626,12 +647,12 @@ __global__ void __launch_bounds__(64 * NW)
         }
         // boundary rows for step p+1: stage 1's centre is in(p), stage s's is t_{s-1}(p-s+1)
         if constexpr (!DB) __syncthreads();  // single buffer: every read of it is done
-        *reinterpret_cast<VT*>(&L[P][0][w][0][xl]) = vin[S % NS][0];
-        *reinterpret_cast<VT*>(&L[P][0][w][1][xl]) = vin[S % NS][RY - 1];
+        *reinterpret_cast<VT*>(&L[P][0][vw][0][xl]) = vin[S % NS][0];
+        *reinterpret_cast<VT*>(&L[P][0][vw][1][xl]) = vin[S % NS][RY - 1];
 #pragma unroll
         for (int s = 2; s <= K; ++s) {  // t_{s-1}(p-s+1), now in H
-            *reinterpret_cast<VT*>(&L[P][s - 1][w][0][xl]) = hget(s - 1, (S - s + 5) & 1, 0);
-            *reinterpret_cast<VT*>(&L[P][s - 1][w][1][xl]) = hget(s - 1, (S - s + 5) & 1, RY - 1);
+            *reinterpret_cast<VT*>(&L[P][s - 1][vw][0][xl]) = hget(s - 1, (S - s + 5) & 1, 0);
+            *reinterpret_cast<VT*>(&L[P][s - 1][vw][1][xl]) = hget(s - 1, (S - s + 5) & 1, RY - 1);
         }
         if constexpr (SIG) {
             // right after the store of a face's last plane (the host makes
@@ -746,11 +767,11 @@ __global__ void __launch_bounds__(64 * NW)
 int senv_int(const char* name, int dflt) { return knob(name, dflt); }
 
 template <typename T, int V, int RY, int NW, int K, bool DB = true, int DIAG = 0, bool SIG = false, int NS = 4,
-          bool FP = true, bool HL = false>
+          bool FP = true, bool HL = false, bool SPLIT = false>
 int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, hipStream_t s,
               unsigned* sig = nullptr, int* nsig = nullptr, unsigned long long* fsig = nullptr,
               const StripGate& gate = StripGate{}) {
-    using Tl = StripTile<T, V, RY, NW, K, DB>;
+    using Tl = StripTile<T, V, RY, NW, K, DB, SPLIT>;
     static_assert(Tl::lds_bytes + (HL ? size_t(2) * Tl::RH * Tl::RW * sizeof(T) : 0) <= 160 * 1024, "LDS budget");
     const Geom g = geom_of(l);
     const int64_t nz = end - begin;
@@ -758,7 +779,7 @@ int launch_st(const stencil_layout& l, const void* in, void* out, int64_t begin,
     if ((g.plane + g.row + 64) * int64_t(sizeof(T)) >= (int64_t(1) << 32) || g.nz + 2 * K >= (int64_t(1) << 30))
         return set_error(STENCIL_EINVAL, "plane too large for tkstrip (4 GiB per plane, 2^30 planes)");
     const int64_t gx = (g.nx + Tl::TX - 1) / Tl::TX, gy = (g.ny + Tl::TY - 1) / Tl::TY;
-    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP, HL>;
+    auto kern = tkstrip_7pt<T, V, RY, NW, K, DB, DIAG, SIG, NS, FP, HL, false, SPLIT>;
     const int64_t tiles = gx * gy;
     int dev = 0, slots = 0;
     STENCIL_HIP_CHECK(hipGetDevice(&dev));
@@ -1051,7 +1072,15 @@ int tier_end(TierJob* j, hipStream_t s, bool* failed) {
 #endif
 int STRIP_ILP_FN(const stencil_layout& l, const void* in, void* out, int64_t begin, int64_t end, int steps,
                  hipStream_t s) {
+#ifdef TK_PROBE_SPLIT64
+    if (l.prob.dtype == STENCIL_F64 && steps == 4)
+        return launch_st<double, 2, TK_PROBE_SPLIT64, 8, 4, false, 0, false, 4, true, true, true>(l, in, out, begin, end, s);
+#endif
     if (l.prob.dtype == STENCIL_F64 && steps == 4) return launch_st<double, 1, 7, 8, 4>(l, in, out, begin, end, s);
+#ifdef TK_PROBE_SPLIT
+    if (l.prob.dtype == STENCIL_F32 && steps == 5)
+        return launch_st<float, 4, TK_PROBE_SPLIT, 8, 5, false, 0, false, 4, true, true, true>(l, in, out, begin, end, s);
+#endif
     if (l.prob.dtype == STENCIL_F32 && steps == 5)
         return launch_st<float, 2, 5, 8, 5, true, 0, false, TK_ILP_NS32>(l, in, out, begin, end, s);
     return set_error(STENCIL_EINVAL, "no max-ILP strip shape for %d steps", steps);
@@ -1437,6 +1466,10 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             // stage 1's history in LDS (HL): 8-row strips at K = 4
             case 810808: return launch_st<double, 1, 8, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
             case 810708: return launch_st<double, 1, 7, 8, 4, true, 0, false, 4, true, true>(l, in, out, begin, end, s);
+            // SPLIT (two strips per wave, 32 lanes x 2 cells: 16-B lane loads): 64 x 64 / 64 x 48 regions
+            case 1020408: return launch_st<double, 2, 4, 8, 4, true, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1020308: return launch_st<double, 2, 3, 8, 4, true, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1820408: return launch_st<double, 2, 4, 8, 4, false, 0, false, 4, true, true, true>(l, in, out, begin, end, s);
             // 9-row strips without the fast path: 72 rows for 64 output rows (512 = 8 x 64)
             case 820908: return launch_st<double, 1, 9, 8, 4, true, 0, false, 4, false, true>(l, in, out, begin, end, s);
             default:
@@ -1458,6 +1491,18 @@ int launch_tkstrip(const stencil_layout& l, const void* in, void* out, int64_t b
             // input planes loaded 3 / 4 planes ahead (NS = 5 / 6) instead of 2
             case 520508: return launch_st<float, 2, 5, 8, 5, true, 0, false, 5>(l, in, out, begin, end, s);
             case 620508: return launch_st<float, 2, 5, 8, 5, true, 0, false, 6>(l, in, out, begin, end, s);
+            // 4 cells per lane (256-wide regions: 16-B lane loads), one boundary-row buffer (80 KB of LDS)
+            case 40408: return launch_st<float, 4, 4, 8, 5, false>(l, in, out, begin, end, s);
+            case 840408: return launch_st<float, 4, 4, 8, 5, false, 0, false, 4, true, true>(l, in, out, begin, end, s);
+            // SPLIT (two strips per wave, 32 lanes x 4 cells: 16-B lane loads): 128 x 32 / 128 x 48 regions
+            case 1040208: return launch_st<float, 4, 2, 8, 5, true, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1040308: return launch_st<float, 4, 3, 8, 5, true, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1030308: return launch_st<float, 4, 3, 8, 5, false, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1030212: return launch_st<float, 4, 2, 12, 5, false, 0, false, 4, true, false, true>(l, in, out, begin, end, s);
+            case 1830308: return launch_st<float, 4, 3, 8, 5, false, 0, false, 4, true, true, true>(l, in, out, begin, end, s);
+            case 1830408: return launch_st<float, 4, 4, 8, 5, false, 0, false, 4, true, true, true>(l, in, out, begin, end, s);
+            // the same, 5-row strips with stage 1's history in LDS (160 KB)
+            case 840508: return launch_st<float, 4, 5, 8, 5, false, 0, false, 4, true, true>(l, in, out, begin, end, s);
             default: return launch_tkstrip_ilp(l, in, out, begin, end, 5, s);
             }
         }

@@ -4,8 +4,13 @@
 // library builds timed in separate processes also differ in where the grids
 // land in physical memory, which moves the fp32 strip by up to 7 % with
 // bit-identical kernel code.  Linked into the debug library
-// only.  Now: a control, the same code as kernels_strip_ilp.hip.
+// only.  Now: the fp32 K = 5 SPLIT shape (two 3-row strips per wave, 16-B
+// lane vectors, stage 1's history in LDS, one boundary buffer) under the
+// max-ILP scheduler; fp64 K = 4 the same with two 4-row strips of 32 lanes x 2
+// cells.
 #define STRIP_ILP_TU
 #define STRIP_ILP_FN launch_tkstrip_probe
 #define TK_ILP_NS32 4
+#define TK_PROBE_SPLIT 3
+#define TK_PROBE_SPLIT64 4
 #include "kernels_strip.hip"

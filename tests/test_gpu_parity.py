@@ -285,7 +285,11 @@ def test_temporalk_chunking(gpu, monkeypatch, steps, cfg, zchunk, dtype):
                                          ("4", "710708"),
                                          # the default shapes from kernels_strip.hip's own build ("1": AUTO, the
                                          # max-ILP build kernels_strip_ilp.hip on these small grids)
-                                         ("5", "20508")])
+                                         ("5", "20508"),
+                                         # SPLIT: two strips per wave, 16-B lane vectors (fp32 4 / fp64 2 cells
+                                         # per lane; each cfg is one dtype's shape, the other dtype runs AUTO)
+                                         ("5", "1040208"), ("5", "1030308"), ("5", "1830308"), ("5", "1030212"),
+                                         ("4", "1020408"), ("4", "1020308"), ("4", "1820408")])
 @pytest.mark.parametrize("zchunk", ["0", "4", "7", "16"])
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("shape3", [(131, 61, 29), (64, 7, 9), (250, 100, 12)])
