@@ -76,6 +76,20 @@
 #ifndef TK_PROBE_NOBAR
 #define TK_PROBE_NOBAR 0
 #endif
+// TK_SST (kernels_strip_probe.hip only, an experiment): the fp32 two-cells-per-
+// lane strip stores its output planes as 16-B lane vectors staged through an
+// LDS image of the wave's own rows (ds_write_b64 per row, ds_read_b128 per row
+// pair: lanes 0..31 row 2i, 32..63 row 2i+1), with an 8-cell x ring so every
+// stored lane vector is whole inside the tile
+#ifndef TK_SST
+#define TK_SST 0
+#endif
+// TK_XRING8 (kernels_strip_probe.hip only, an experiment): the fp32 two-cells-
+// per-lane strip with an 8-cell x ring (TX = 112), so regions start on a 32-B
+// boundary
+#ifndef TK_XRING8
+#define TK_XRING8 0
+#endif
 
 namespace stencil {
 namespace {
@@ -131,7 +145,9 @@ template <typename T, int V, int RY, int NW, int K, bool DB, bool SPLIT = false>
 struct StripTile {
     static constexpr int LW = SPLIT ? 32 : 64;       // lanes per strip row
     static constexpr int NSTR = SPLIT ? 2 * NW : NW; // strips per region
-    static constexpr int XR = (K + V - 1) / V;  // ring vectors per x side
+    static constexpr bool SSTS = TK_SST && sizeof(T) == 4 && V == 2 && !SPLIT;  // TK_SST staged stores
+    static constexpr bool XR8 = (SSTS || TK_XRING8) && sizeof(T) == 4 && V == 2 && !SPLIT;
+    static constexpr int XR = XR8 ? 8 / V : (K + V - 1) / V;  // ring vectors per x side
     static constexpr int RW = LW * V;           // region width
     static constexpr int TX = RW - 2 * XR * V;  // output tile width
     static constexpr int RH = NSTR * RY;        // region height
@@ -258,6 +274,10 @@ __global__ void __launch_bounds__(64 * NW)
     constexpr int XR = Tl::XR, TX = Tl::TX, TY = Tl::TY, RH = Tl::RH, RW = Tl::RW, NB = Tl::NB;
     constexpr int LW = Tl::LW, NSTR = Tl::NSTR;
     static_assert(!SPLIT || !TIER, "SPLIT: plain or face-signalled launches");
+    constexpr bool SST = Tl::SSTS && !SIG && !TIER && !HL;
+    constexpr int NI = (RY + 1) / 2;  // SST: row pairs per strip
+    typedef T V4T __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) T IMG[SST ? RH : 1][SST ? RW : 1];
     static_assert(TY > 0 && TX > 0, "tile too small for K");
     static_assert(RY >= 2, "a strip needs a first and a last row");
     static_assert(!HL || K >= 2, "HL keeps stage 1's history");
@@ -394,6 +414,25 @@ __global__ void __launch_bounds__(64 * NW)
         off[k] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
         yin[k] = y >= 0 && y < g.ny;
         st[k] = rr >= K && rr < RH - K && y < g.ny && hl >= XR && hl < LW - XR;
+    }
+    // SST: the 16-B store lanes (cells 4(l%32) .. +3 of strip row 2i + l/32)
+    uint32_t soff[SST ? NI : 1];
+    bool sfull[SST ? NI : 1], spart[SST ? NI : 1];
+    const int64_t xs = int64_t(bx) * TX - XR * V + 4 * int64_t(lane & 31);
+    if constexpr (SST) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int kk = 2 * i + (lane >> 5);
+            const int rr = w * RY + kk;
+            const int64_t y = y0 + kk;
+            const bool ok = kk < RY && rr >= K && rr < RH - K && y < g.ny && 4 * (lane & 31) >= XR * V &&
+                            4 * (lane & 31) < RW - XR * V;
+            const int64_t yc = y < 0 ? 0 : (y > g.ny ? g.ny : y);
+            const int64_t xc = xs < 0 ? 0 : (xs > g.nx ? g.nx : xs);
+            soff[i] = uint32_t((yc * g.row + xc + bias) * int64_t(sizeof(T)));
+            sfull[i] = ok && xs + 3 < g.nx;
+            spart[i] = ok && xs < g.nx && xs + 3 >= g.nx;
+        }
     }
     bool xin[V], xst[V];
 #pragma unroll
@@ -634,6 +673,10 @@ __global__ void __launch_bounds__(64 * NW)
                                       off[k], prev);
                 continue;
             }
+            if constexpr (SST) {
+                if (do_store) *reinterpret_cast<VT*>(&IMG[w * RY + k][xl]) = prev;
+                continue;
+            }
             if (do_store && st[k]) {
                 T* q = reinterpret_cast<T*>(obase + off[k]);
                 if (xst[V - 1]) {
@@ -643,6 +686,27 @@ __global__ void __launch_bounds__(64 * NW)
                     for (int j = 0; j < V; ++j)
                         if (xst[j]) q[j] = prev[j];
                 }
+            }
+        }
+        if constexpr (SST) {
+            // the wave's own image rows back as 16-B lane vectors (LDS ops of one
+            // wave execute in order; the asm keeps the compiler from moving them)
+            if (do_store) {
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const int kk = 2 * i + (lane >> 5) < RY ? 2 * i + (lane >> 5) : RY - 1;
+                    const V4T v = *reinterpret_cast<const V4T*>(&IMG[w * RY + kk][4 * (lane & 31)]);
+                    T* q = reinterpret_cast<T*>(obase + soff[i]);
+                    if (sfull[i]) {
+                        __builtin_nontemporal_store(v, reinterpret_cast<V4T*>(q));
+                    } else if (spart[i]) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xs + j < g.nx) q[j] = v[j];
+                    }
+                }
+                asm volatile("" ::: "memory");
             }
         }
         // boundary rows for step p+1: stage 1's centre is in(p), stage s's is t_{s-1}(p-s+1)

@@ -4,13 +4,10 @@
 // library builds timed in separate processes also differ in where the grids
 // land in physical memory, which moves the fp32 strip by up to 7 % with
 // bit-identical kernel code.  Linked into the debug library
-// only.  Now: the fp32 K = 5 SPLIT shape (two 3-row strips per wave, 16-B
-// lane vectors, stage 1's history in LDS, one boundary buffer) under the
-// max-ILP scheduler; fp64 K = 4 the same with two 4-row strips of 32 lanes x 2
-// cells.
+// only.  Now: TK_XRING8, the fp32 K = 5 default shape with an 8-cell x ring
+// (regions on 32-B boundaries; kernels_strip.hip).
 #define STRIP_ILP_TU
 #define STRIP_ILP_FN launch_tkstrip_probe
 #define TK_ILP_NS32 4
-#define TK_PROBE_SPLIT 3
-#define TK_PROBE_SPLIT64 4
+#define TK_XRING8 1
 #include "kernels_strip.hip"

@@ -287,6 +287,90 @@ __global__ void __launch_bounds__(512) march_glds(const float* __restrict__ in, 
     sink[w * 64 + lane] = acc;  // keep the loads alive
 }
 
+// STAGED STORES: the V = 2 register layout (8-B loads straight to registers,
+// as `ring`), but each output plane goes to an LDS image of the wave's own
+// rows (ds_write_b64) and leaves as 16-B lane vectors (ds_read_b128: lanes
+// 0..31 row 2i, 32..63 row 2i+1) -- no barrier (a wave reads back only its own
+// rows).  x ring 8 cells (TX = 112), so every stored lane vector is whole.
+template <int RY>
+__global__ void __launch_bounds__(512) march_sst(const float* __restrict__ in, float* __restrict__ out, int tiles_x,
+                                                 int tiles_y, int xcd_pw) {
+    constexpr int NW = 8, DELAY = 5, TX = 112, RX = 8, RYR = 5, TY = NW * RY - 2 * RYR, NI = (RY + 1) / 2;
+    typedef float VT __attribute__((ext_vector_type(2)));
+    typedef float V4 __attribute__((ext_vector_type(4)));
+    const long tiles = long(tiles_x) * tiles_y;
+    long t = blockIdx.x;
+    if (xcd_pw > 0) {
+        const long per = (tiles + 7) / 8;
+        const long u = long(blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (u >= tiles) return;
+        const long strip = u / (long(xcd_pw) * tiles_y), rem = u - strip * xcd_pw * tiles_y;
+        const long sw = tiles_x - strip * xcd_pw < xcd_pw ? tiles_x - strip * xcd_pw : xcd_pw;
+        t = rem / sw * tiles_x + strip * xcd_pw + rem % sw;
+    }
+    if (t >= tiles) return;
+    const int bx = int(t % tiles_x), by = int(t / tiles_x);
+    const int lane = threadIdx.x, w = threadIdx.y;
+    __shared__ __attribute__((aligned(16))) float img[NW * RY][128];
+    const long x = long(bx) * TX - RX + 2 * lane;
+    long off[RY];
+#pragma unroll
+    for (int k = 0; k < RY; ++k) {
+        const long y = long(by) * TY - RYR + w * RY + k;
+        const long yc = y < -1 ? -1 : (y > NY ? NY : y);
+        const long xc = x < -2 ? -2 : (x > NX ? NX : x);
+        off[k] = ORIGIN + yc * ROW + xc;
+    }
+    // 16-B store lanes: cells 4(l%32) .. +3 of row 2i + l/32
+    const long xs = long(bx) * TX - RX + 4 * (lane % 32);
+    long soff[NI];
+    bool sst[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int k = 2 * i + lane / 32;
+        const int rr = w * RY + k;
+        const long y = long(by) * TY - RYR + rr;
+        sst[i] = k < RY && rr >= RYR && rr < NW * RY - RYR && y >= 0 && y < NY && 4 * (lane % 32) >= RX &&
+                 4 * (lane % 32) < 128 - RX && xs >= 0 && xs + 3 < NX;
+        soff[i] = ORIGIN + (y < 0 ? 0 : y) * ROW + (xs < 0 ? 0 : xs);
+    }
+    __shared__ float sink[64 * NW];
+    VT ring[4][RY];
+    auto load = [&](VT(&d)[RY], int z) {
+        const int zz = z < -1 ? -1 : (z > NZ ? NZ : z);
+#pragma unroll
+        for (int k = 0; k < RY; ++k) d[k] = *reinterpret_cast<const VT*>(in + zz * PLANE + off[k]);
+    };
+    const int za = 0, zb = NZ;
+    load(ring[0], za - DELAY);
+    load(ring[1], za - DELAY + 1);
+    float acc = 0;
+    auto step = [&](auto S_, int p) {
+        constexpr int S = decltype(S_)::value;
+        __syncthreads();
+        const int zo = p - DELAY;
+        if (zo >= za && zo < zb) {
+#pragma unroll
+            for (int k = 0; k < RY; ++k) *reinterpret_cast<VT*>(&img[w * RY + k][2 * lane]) = ring[(S + 2) % 4][k];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const V4 v = *reinterpret_cast<const V4*>(&img[w * RY + (2 * i + lane / 32 < RY ? 2 * i + lane / 32 : 0)][4 * (lane % 32)]);
+                if (sst[i]) __builtin_nontemporal_store(v, reinterpret_cast<V4*>(out + zo * PLANE + soff[i]));
+            }
+        }
+        acc += ring[S][0][0];
+        load(ring[(S + 2) % 4], p + 2);
+    };
+    int p = za - DELAY;
+    for (; p + 3 <= zb + DELAY; p += 4) {
+        step(std::integral_constant<int, 0>{}, p);
+        step(std::integral_constant<int, 1>{}, p + 1);
+        step(std::integral_constant<int, 2>{}, p + 2);
+        step(std::integral_constant<int, 3>{}, p + 3);
+    }
+    sink[w * 64 + lane] = acc;  // keep the loads alive
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 5;
     const long elems = PLANE * PLANES + 256;
@@ -335,6 +419,18 @@ int main(int argc, char** argv) {
             geo("tile 128x40 (no over-fetch)", march<2, 5, 8, 5>, 8, 128, 40, 0, 0, pw);
             geo("wide 256x40 -> 240x30", march<4, 5, 8, 5>, 8, 240, 30, 8, 5, pw);
             geo("tall 128x80 -> 116x70 (16 waves)", march<2, 5, 16, 5>, 16, 116, 70, 6, 5, pw);
+        }
+    } else if (mode == 4) {
+        // the V = 2 register layout with 16-B stores staged through LDS (x ring 8: TX = 112)
+        for (int pw : {16, 0}) {
+            geo("ring 128x40 -> 116x30, K=5", march<2, 5, 8, 5>, 8, 116, 30, 6, 5, pw);
+            geo("ring8 128x40 -> 112x30 (x ring 8)", march<2, 5, 8, 5>, 8, 112, 30, 8, 5, pw);
+            const int gx = (NX + 111) / 112, gy = (NY + 29) / 30;
+            const long n = pw > 0 ? (long(gx) * gy + 7) / 8 * 8 : long(gx) * gy;
+            timeit(pw ? "sst RY5 16-B stores via LDS (XCD patch)" : "sst RY5 16-B stores via LDS (tile-major)", comp, [&] {
+                hipLaunchKernelGGL(march_sst<5>, dim3(unsigned(n)), dim3(64, 8), 0, 0, a, b, gx, gy, pw);
+            });
+            geo("pair 128x48 -> 112x38, 16-B loads", march_pair<3, 8, 5>, 8, 112, 38, 8, 5, pw);
         }
     } else if (mode == 3) {
         // the ring geometry with LDS-DMA 16-B input loads (register layout kept)
