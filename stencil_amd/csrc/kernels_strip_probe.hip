@@ -4,10 +4,10 @@
 // library builds timed in separate processes also differ in where the grids
 // land in physical memory, which moves the fp32 strip by up to 7 % with
 // bit-identical kernel code.  Linked into the debug library
-// only.  Now: TK_XRING8, the fp32 K = 5 default shape with an 8-cell x ring
-// (regions on 32-B boundaries; kernels_strip.hip).
+// only.  Now a control (the same code as kernels_strip_ilp.hip); round 6 built
+// it with TK_PROBE_NOBAR, TK_PROBE_SPLIT(64), TK_SST, TK_XRING8 and under the
+// gcn-iterative-ilp scheduler (profiles/r06/r06q_* .. r06w_*).
 #define STRIP_ILP_TU
 #define STRIP_ILP_FN launch_tkstrip_probe
 #define TK_ILP_NS32 4
-#define TK_XRING8 1
 #include "kernels_strip.hip"
