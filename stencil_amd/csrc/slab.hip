@@ -199,8 +199,13 @@ struct HipDev {
         return STENCIL_OK;
     }
     static void free(void* p) { (void)hipFree(p); }
+    // hipMemset runs on the null stream, which the job's non-blocking streams
+    // do not follow: the zeroes must land before any of their launches adds
+    // to the counters (or a face wait waits for a count the memset erased),
+    // so the host waits for them here (creation / reset: the streams are idle)
     static int alloc_counters(uint32_t** c) {
-        if (hipMalloc(c, 4 * sizeof(uint32_t)) != hipSuccess || hipMemset(*c, 0, 4 * sizeof(uint32_t)) != hipSuccess)
+        if (hipMalloc(c, 4 * sizeof(uint32_t)) != hipSuccess || hipMemset(*c, 0, 4 * sizeof(uint32_t)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
             return set_error(STENCIL_EHIP, "face counters");
         return STENCIL_OK;
     }
@@ -218,10 +223,10 @@ struct HipDev {
     static int reset_counters(uint32_t* c, uint32_t* flag, uint64_t* fs) {
         if (c) STENCIL_HIP_CHECK(hipMemset(c, 0, 4 * sizeof(uint32_t)));
         if (flag) __atomic_store_n(flag, 0u, __ATOMIC_SEQ_CST);
-        if (fs) {
+        if (fs)
             if (int rc = stencil_face_signal_reset(fs, nullptr)) return rc;
-            STENCIL_HIP_CHECK(hipDeviceSynchronize());
-        }
+        // the null-stream memset / reset done before the job's streams launch (alloc_counters)
+        if (c || fs) STENCIL_HIP_CHECK(hipDeviceSynchronize());
         return STENCIL_OK;
     }
     // a failed job: let every queued face wait return (the polling kernel
